@@ -1,0 +1,275 @@
+/*
+ * zrt.h — C ABI of the MI355X path tracer (libzrt.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel Monte-Carlo
+ * sampling loop.  The reference seam is
+ *
+ *     pub fn render(allocator: *Allocator, random: *Random,
+ *                   camera: Camera, surfaces: ArrayList(Surface),
+ *                   render_params: RenderParams) !*Image
+ *                                              (src/raytrace.zig:136-138)
+ *
+ * A Zig caller flattens `ArrayList(Surface)` (src/surface.zig:12-16), the
+ * `*const Material` pointers (src/material.zig:16-52), the `Texture` values
+ * (src/texture.zig:7-28) and the `*Image` pointers they reference into the flat
+ * arrays of `zrt_scene`, keeping the reference list order, and calls
+ * `zrt_render`.  See INTEGRATION.md for the `@cImport` adapter.
+ *
+ * Conventions (all from the reference):
+ *   - f32 everywhere (src/base.zig:2).
+ *   - Framebuffer: width*height RGB f32, row-major, row 0 = bottom of the image
+ *     (src/raytrace.zig:164-182, src/image.zig:74-78).
+ *   - Texture images: same layout, already flipped and scaled by 1/255 as
+ *     src/png_image.zig:76-89 produces them.
+ *   - Camera: the four vectors `Camera.init` computes (src/camera.zig:17-35);
+ *     `zrt_camera_init` restates `Camera.init` on the host (tan stays on host).
+ *
+ * Errors: every entry point returns ZRT_OK (0) or a negative ZRT_E_* code and
+ * leaves a message in a thread-local buffer read by `zrt_last_error()`.  This
+ * maps 1:1 onto a Zig error union (`!*Image`).  No C++ exception crosses the ABI.
+ *
+ * Ownership: the library copies every input during the call and keeps no
+ * pointer into caller memory after it returns.  `out_rgb` is caller-allocated.
+ * Device memory is owned by the library (zrt_render) or by a zrt_ctx handle.
+ * The library is not reentrant on one zrt_ctx; distinct contexts may be used
+ * from distinct threads.
+ */
+#ifndef ZRT_H
+#define ZRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZRT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+enum {
+  ZRT_OK = 0,
+  ZRT_E_INVALID = -1,     /* bad argument (e.g. unknown kind, index out of range) */
+  ZRT_E_NOMEM = -2,       /* host or device allocation failed (Zig: OutOfMemory) */
+  ZRT_E_HIP = -3,         /* HIP runtime error */
+  ZRT_E_UNSUPPORTED = -4, /* valid for the reference, not provided by this path */
+  ZRT_E_NODEVICE = -5,    /* no usable MI355X (gfx950) device */
+  ZRT_E_IO = -6,          /* asset file missing / unreadable */
+  ZRT_E_PARSE = -7        /* OBJ parse error (obj_reader.zig ParseError) */
+};
+
+/* ---- scene description (flattened ArrayList(Surface)) ------------------- */
+enum { ZRT_PRIM_SPHERE = 0, ZRT_PRIM_TRIANGLE = 1 };          /* surface.zig:12-16 */
+enum { ZRT_MAT_LAMBERTIAN = 0, ZRT_MAT_METAL = 1, ZRT_MAT_DIELECTRIC = 2 }; /* material.zig:27-29 */
+enum { ZRT_TEX_COLOR = 0, ZRT_TEX_IMAGE = 1 };                /* texture.zig:7-9 */
+
+typedef struct zrt_vec3 { float x, y, z; } zrt_vec3;          /* vector.zig:22-25 */
+
+/* Camera.{origin, lower_left_corner, horizontal, vertical} (camera.zig:11-15). */
+typedef struct zrt_camera {
+  zrt_vec3 origin;
+  zrt_vec3 lower_left_corner;
+  zrt_vec3 horizontal;
+  zrt_vec3 vertical;
+} zrt_camera;
+
+/* One element of ArrayList(Surface).  kind selects the union member:
+ *   SPHERE:   center, radius            (Sphere.init, sphere.zig:24-29)
+ *   TRIANGLE: a, b, c (vertex order kept: Triangle.init, triangle.zig:32-44)
+ * `material` indexes zrt_scene.materials (the deduplicated *const Material). */
+typedef struct zrt_prim {
+  uint32_t kind;
+  uint32_t material;
+  zrt_vec3 center;
+  float radius;
+  zrt_vec3 a, b, c;
+} zrt_prim;
+
+/* Material union (material.zig:16-52).  `texture` indexes zrt_scene.textures
+ * and is used by LAMBERTIAN and METAL; `index_of_refraction` by DIELECTRIC. */
+typedef struct zrt_material {
+  uint32_t kind;
+  uint32_t texture;
+  float index_of_refraction;
+} zrt_material;
+
+/* Texture union (texture.zig:7-28): COLOR uses `color`; IMAGE uses `image`
+ * (index into zrt_scene.images), `u_offset`, `v_offset` (Texture.initImage
+ * passes 0.19, 0.1: texture.zig:14-16). */
+typedef struct zrt_texture {
+  uint32_t kind;
+  uint32_t image;
+  zrt_vec3 color;
+  float u_offset;
+  float v_offset;
+} zrt_texture;
+
+/* Image (image.zig:74-78): width*height RGB f32, row 0 = bottom. */
+typedef struct zrt_image {
+  uint32_t width;
+  uint32_t height;
+  const float* pixels;
+} zrt_image;
+
+typedef struct zrt_scene {
+  const zrt_prim* prims;         /* reference list order (scenes.zig append order) */
+  uint32_t n_prims;
+  uint32_t n_materials;
+  const zrt_material* materials;
+  const zrt_texture* textures;
+  uint32_t n_textures;
+  uint32_t n_images;
+  const zrt_image* images;
+} zrt_scene;
+
+/* ---- render parameters (RenderParams, raytrace.zig:102-108) ------------- */
+enum {
+  ZRT_RNG_COUNTER = 0,          /* per-(pixel,sample) stream; the GPU mode */
+  ZRT_RNG_REFERENCE_STREAM = 1  /* one sequential stream as the reference; CPU oracle only */
+};
+enum { ZRT_PRNG_XOROSHIRO128 = 0, ZRT_PRNG_XOSHIRO256 = 1 };
+enum {
+  ZRT_TRAVERSAL_FAST = 0,       /* near-first, extra conservative slab prune, DFS tie-break */
+  ZRT_TRAVERSAL_REFERENCE = 1   /* left-first DFS with exactly bvh.zig:187-205's tests */
+};
+
+typedef struct zrt_params {
+  uint32_t width;                    /* RenderParams.width (u16 in the reference) */
+  uint32_t height;                   /* RenderParams.height */
+  uint32_t samples_per_pixel;        /* RenderParams.samples_per_pixel */
+  uint32_t max_depth;                /* RenderParams.max_depth */
+  uint32_t bounded_volume_hierarchy; /* RenderParams.bounded_volume_hierarchy (BVH iff also n>10) */
+  uint32_t rng_mode;                 /* ZRT_RNG_* */
+  uint32_t prng;                     /* ZRT_PRNG_* (DefaultPrng variant) */
+  uint32_t traversal;                /* ZRT_TRAVERSAL_* */
+  uint64_t seed;                     /* DefaultPrng.init(seed); the scenes use 42 */
+  uint32_t rank;                     /* image-tile partition: this rank ... */
+  uint32_t world_size;               /* ... of world_size (1 = whole frame) */
+  uint32_t device;                   /* HIP device ordinal */
+  uint32_t flags;                    /* reserved, 0 */
+} zrt_params;
+
+/* Progress counters (raytrace.zig:20-34) + timings. */
+typedef struct zrt_stats {
+  uint64_t recursion_depth_hits;
+  uint64_t reflections;
+  uint64_t background_hits;
+  uint64_t pixels_processed;
+  uint64_t samples_processed;
+  uint64_t rays_processed;
+  uint64_t node_visits;   /* BVH nodes whose box was tested (diagnostic) */
+  uint64_t prim_tests;    /* primitive intersection tests (diagnostic) */
+  double preprocess_ms;   /* BVH build + flatten (raytrace.zig:150) */
+  double upload_ms;
+  double render_ms;       /* kernel time (HIP events) */
+  double gather_ms;
+  uint32_t used_bvh;      /* preprocessSufraces decision (raytrace.zig:124-133) */
+  uint32_t bvh_nodes;
+  uint32_t bvh_max_depth; /* Tracking.max_depth (bvh.zig:23-30) */
+  uint32_t n_gpus;
+} zrt_stats;
+
+/* ---- entry points -------------------------------------------------------- */
+
+/* Replaces raytrace.render (raytrace.zig:136-203): render the whole frame on
+ * one GPU (params->device).  out_rgb: width*height*3 f32, caller-allocated.
+ * rng_mode must be ZRT_RNG_COUNTER.  stats may be NULL. */
+int zrt_render(const zrt_scene* scene, const zrt_camera* camera,
+               const zrt_params* params, float* out_rgb, zrt_stats* stats);
+
+/* Restates Camera.init (camera.zig:17-35).  look_from/look_at/vup: float[3]. */
+int zrt_camera_init(const float look_from[3], const float look_at[3],
+                    const float vup[3], float vfov_deg, float aspect_ratio,
+                    zrt_camera* out);
+
+/* Thread-local message for the last error on this thread ("" if none). */
+const char* zrt_last_error(void);
+
+/* ABI version (ZRT_ABI_VERSION) and build identity string. */
+int zrt_abi_version(void);
+const char* zrt_build_info(void);
+
+/* ---- device-resident context (bench / multi-GPU) ------------------------ *
+ * zrt_ctx_create does preprocessSufraces (BVH build, raytrace.zig:124-133),
+ * flattens the scene and uploads it once to params->device.  zrt_ctx_render
+ * then runs only the sampling loop, reading the resident scene and writing a
+ * device buffer, so a timed region sees no host<->device traffic.           */
+typedef struct zrt_ctx zrt_ctx;
+
+int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** out);
+int zrt_ctx_destroy(zrt_ctx* ctx);
+
+/* Number of 8x8 tiles this (rank, world_size) owns; its tile buffer holds
+ * n_tiles*64*3 floats.  Tiles are dealt round-robin: tile t -> rank t % world. */
+int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n_tiles);
+
+/* Render this rank's tiles into dev_tiles (device pointer, tile-major,
+ * n_tiles*64*3 f32) on `hip_stream` (hipStream_t, NULL = default stream).
+ * Asynchronous: returns after enqueueing; counters are produced by
+ * zrt_ctx_stats after the stream is synchronised. */
+int zrt_ctx_render_tiles(zrt_ctx* ctx, const zrt_camera* camera,
+                         const zrt_params* params, float* dev_tiles,
+                         void* hip_stream);
+
+/* Scatter gathered tiles of all ranks (rank-major: rank r's n_tiles(r) tiles
+ * follow rank r-1's) into the framebuffer layout of raytrace.zig:182.
+ * dev_gathered / dev_frame are device pointers; runs on hip_stream. */
+int zrt_ctx_assemble(zrt_ctx* ctx, const zrt_params* params,
+                     const float* dev_gathered, float* dev_frame, void* hip_stream);
+
+/* Counters of the last zrt_ctx_render_tiles (synchronises the ctx stream). */
+int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
+
+/* Duration in ms of the last zrt_ctx_render_tiles' kernel (HIP events on the
+ * launch stream; synchronises). */
+int zrt_ctx_last_kernel_ms(zrt_ctx* ctx, double* ms);
+
+/* ---- host-side scene ingestion (the caller side of the seam) ------------- *
+ * Restatement of scenes.zig / obj_reader.zig / png_image.zig texture loading
+ * so tests and bench can build the reference's scenes without Zig.  Assets are
+ * read from `assets_dir` (OBJ files and P6 PPM textures, tools/prepare_assets.py). */
+typedef struct zrt_scene_data zrt_scene_data;
+
+/* Build scene `scene_index` as scenes.zig:267-277 does (0 man+ball, 1 seven
+ * spheres, 2 bunny+ball, 3 teapot+ball, 4 teapot+ball circle, 5 goat).  The
+ * camera is returned in *camera; the scene view stays valid until
+ * zrt_scene_free.  Unknown index -> ZRT_E_INVALID (SceneError.UnkownSceneIndex). */
+int zrt_scene_load(uint32_t scene_index, const char* assets_dir,
+                   zrt_scene_data** out, zrt_camera* camera);
+const zrt_scene* zrt_scene_view(const zrt_scene_data* data);
+void zrt_scene_free(zrt_scene_data* data);
+
+/* Parse an OBJ file into triangles (obj_reader.zig:114-198), all with material
+ * `material`.  *out_prims is malloc'd; free with zrt_free. */
+int zrt_obj_read(const char* path, uint32_t material, zrt_prim** out_prims, uint32_t* n_prims);
+void zrt_free(void* p);
+
+/* ---- BVH export (parity of bvh.zig:62-185 against the oracle) ------------- *
+ * Node i: box min/max and two children.  A child c >= 0 is a node index; a
+ * child c < 0 is primitive (-c - 1) in reference list order.  Leaves are
+ * exactly the reference's (one prim on both sides, or s[1], s[0]).  The root
+ * is node 0; nodes are in depth-first (left-first) pre-order. */
+typedef struct zrt_bvh_node {
+  zrt_vec3 min;
+  int32_t left;
+  zrt_vec3 max;
+  int32_t right;
+} zrt_bvh_node;
+
+int zrt_bvh_build(const zrt_scene* scene, zrt_bvh_node** out_nodes,
+                  uint32_t* n_nodes, uint32_t* max_depth);
+
+/* ---- device parity probes ------------------------------------------------ *
+ * Evaluate the kernel's own device functions on inputs, for bit-exact
+ * comparison with the oracle's restatements:
+ *   fn 0 sin, 1 cos (std.math, Go/Cephes), 2 acos, 3 atan (musl), 4 sqrt,
+ *   5 atan2(x[i], y[i]), 6 pow(x[i], 5.0), 7 x[i] / y[i].
+ * zrt_debug_rng writes n outputs of DefaultPrng.init(key).next() computed on
+ * the device.  Both run on `device` and synchronise. */
+int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t n, uint32_t device);
+int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZRT_H */

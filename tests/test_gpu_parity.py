@@ -1,0 +1,197 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar: bit-exact.  In counter-RNG mode the kernel and the oracle draw the same
+random numbers and execute the same f32 operations (both -ffp-contract=off,
+both with correctly rounded div/sqrt and the same restated transcendentals),
+so images and progress counters must be identical — NaN compares equal to NaN.
+
+Run on an MI355X: ``pytest -m gpu``.
+"""
+import numpy as np
+import pytest
+
+import zraytrace_amd as z
+from oracle import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+COUNTERS = ("recursion_depth_hits", "reflections", "background_hits", "rays_processed",
+            "pixels_processed", "samples_processed")
+
+
+def same_bits(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    nan = np.isnan(a) & np.isnan(b)
+    eq = (a.view(np.uint32) == b.view(np.uint32)) | nan
+    return eq
+
+
+def assert_bit_exact(gpu, ref):
+    eq = same_bits(gpu, ref)
+    if not eq.all():
+        bad = np.argwhere(~eq.reshape(gpu.shape[0], gpu.shape[1], 3).all(axis=2))
+        y, x = bad[0]
+        raise AssertionError(f"{len(bad)} pixels differ; first at (x={x}, y={y}): "
+                             f"gpu={gpu[y, x]} oracle={ref[y, x]}; max|d|="
+                             f"{np.nanmax(np.abs(gpu - ref))}")
+
+
+# ---- device building blocks ---------------------------------------------------
+
+@pytest.mark.parametrize("prng", [z.ZRT_PRNG_XOROSHIRO128, z.ZRT_PRNG_XOSHIRO256])
+def test_device_rng_matches_oracle(golden, prng):
+    for key in (0, 42, 0x123456789ABCDEF, int(golden["streams"]["counter_keys_seed42"][3]["key"])):
+        np.testing.assert_array_equal(z.debug_rng(prng, key, 64), O.prng_u64(prng, key, 64))
+
+
+def test_device_math_bit_exact():
+    rng = np.random.default_rng(7)
+    n = 4096
+    phi = (np.float32(6.2831855) * rng.random(n, dtype=np.float32)).astype(np.float32)
+    for fn, name in ((0, "sin"), (1, "cos")):
+        assert same_bits(z.debug_math(fn, phi), O.math1(name, phi)).all(), name
+    c = np.concatenate([rng.uniform(-1, 1, n).astype(np.float32),
+                        np.array([-1, 1, 0, -0.0, 0.5, -0.5, 1e-9, 1.0000001, np.nan], np.float32)])
+    assert same_bits(z.debug_math(2, c), O.math1("acos", c)).all(), "acos"
+    a = np.concatenate([rng.normal(0, 5, n).astype(np.float32), np.array([0, 1e30, -1e-30], np.float32)])
+    assert same_bits(z.debug_math(3, a), O.math1("atan", a)).all(), "atan"
+    ys, xs = rng.uniform(-1, 1, n).astype(np.float32), rng.uniform(-1, 1, n).astype(np.float32)
+    ys[:4] = [0, -0.0, 1, 0]
+    xs[:4] = [-1, -1, 0, 1]
+    assert same_bits(z.debug_math(5, ys, xs), O.math2("atan2", ys, xs)).all(), "atan2"
+    p = np.concatenate([rng.random(n, dtype=np.float32), np.array([0, 1, 2, 1e-7, 2 ** -24], np.float32)])
+    assert same_bits(z.debug_math(6, p), O.math2("pow", p, np.full_like(p, 5.0))).all(), "pow5"
+    # IEEE correctly rounded sqrt and division (HIP's default for f32)
+    s = np.abs(rng.normal(0, 100, n)).astype(np.float32)
+    assert same_bits(z.debug_math(4, s), np.sqrt(s)).all(), "sqrt"
+    den = rng.normal(0, 3, n).astype(np.float32)
+    assert same_bits(z.debug_math(7, a[:n], den), (a[:n] / den).astype(np.float32)).all(), "div"
+
+
+# ---- whole-frame parity ---------------------------------------------------------
+
+CASES = [
+    # (scene, width, height, spp, depth)
+    (1, 48, 48, 8, 30),    # seven spheres, list mode (C1/C2 scene)
+    (2, 32, 32, 4, 20),    # bunny + ball, BVH (C4 scene)
+    (3, 32, 32, 4, 20),    # teapot + ball (C3 scene)
+    (4, 24, 24, 4, 20),    # teapot + ball circle: image-textured lambertian, hollow metal sphere
+    (0, 24, 24, 4, 20),    # man + ball
+]
+
+
+@pytest.mark.parametrize("traversal", [z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE])
+@pytest.mark.parametrize("case", CASES, ids=[f"scene{c[0]}" for c in CASES])
+def test_render_bit_exact_vs_oracle(scenes, case, traversal):
+    idx, w, h, spp, depth = case
+    s = scenes(idx)
+    p = z.RenderParams(w, h, spp, depth, traversal=traversal)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+    if traversal == z.ZRT_TRAVERSAL_REFERENCE and rs["used_bvh"]:
+        # the same DFS with the same slab tests visits the same nodes
+        assert gs["node_visits"] == rs["node_visits"]
+
+
+def test_nonsquare_and_ragged_tiles(scenes):
+    """height < width: raytrace.zig:168 leaves columns x >= height black; 8x8
+    tiles overhang both edges (37 x 21)."""
+    s = scenes(1)
+    p = z.RenderParams(37, 21, 3, 12)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    assert np.all(gpu[:, 21:] == 0)
+    assert gs["pixels_processed"] == 21 * 21 == rs["pixels_processed"]
+
+
+@pytest.mark.parametrize("max_depth", [0, 1, 2])
+def test_shallow_depths(scenes, max_depth):
+    """depth <= 0 returns black and counts a recursion-limit hit (raytrace.zig:64-68)."""
+    s = scenes(2)
+    p = z.RenderParams(16, 16, 2, max_depth)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+
+
+def test_xoshiro_and_seed(scenes):
+    s = scenes(1)
+    for prng, seed in ((z.ZRT_PRNG_XOSHIRO256, 42), (z.ZRT_PRNG_XOROSHIRO128, 7)):
+        p = z.RenderParams(24, 24, 4, 30, prng=prng, seed=seed)
+        assert_bit_exact(z.render(s, s.camera, p)[0], O.render(s.view, s.camera, p)[0])
+
+
+def test_no_bvh_flag_uses_list(scenes):
+    """bounded_volume_hierarchy = false: the surface list path on a mesh scene."""
+    s = scenes(4)
+    p = z.RenderParams(8, 8, 2, 6, bounded_volume_hierarchy=False)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert gs["used_bvh"] == 0
+    assert_bit_exact(gpu, ref)
+
+
+def test_deterministic(scenes):
+    s = scenes(2)
+    p = z.RenderParams(64, 64, 8, 20)
+    a, _ = z.render(s, s.camera, p)
+    b, _ = z.render(s, s.camera, p)
+    assert same_bits(a, b).all()
+
+
+# ---- tile partition (multi-GPU path on one device) ----------------------------------
+
+def render_partitioned(scene, p_base, world):
+    import torch
+    ctx = z.RenderContext(scene, p_base)
+    parts = []
+    for rank in range(world):
+        p = z.RenderParams(**{**p_base.__dict__, "rank": rank, "world_size": world})
+        n = ctx.tile_count(p)
+        buf = torch.empty(n * 64 * 3, dtype=torch.float32, device="cuda")
+        ctx.render_tiles(scene.camera, p, buf.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        parts.append(buf)
+    gathered = torch.cat(parts)
+    pw = z.RenderParams(**{**p_base.__dict__, "rank": 0, "world_size": world})
+    frame = torch.empty(p_base.height * p_base.width * 3, dtype=torch.float32, device="cuda")
+    ctx.assemble(pw, gathered.data_ptr(), frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = frame.cpu().numpy().reshape(p_base.height, p_base.width, 3)
+    ctx.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tile_partition_invariance(scenes, world):
+    """1 vs N ranks: bitwise-identical frames (SURVEY §8c protocol 2)."""
+    s = scenes(2)
+    p = z.RenderParams(40, 40, 4, 20)
+    one = render_partitioned(s, p, 1)
+    many = render_partitioned(s, p, world)
+    assert same_bits(one, many).all()
+    assert_bit_exact(one, O.render(s.view, s.camera, p)[0])
+
+
+# ---- the bench configuration, checked through size-independent properties ----------
+
+def test_bench_config_properties(scenes):
+    """Bunny at the bench's 2048^2 resolution (16 spp here): counter identities,
+    value range, and bit-exact rows against the oracle."""
+    s = scenes(2)
+    p = z.RenderParams(2048, 2048, 16, 20)
+    img, st = z.render(s, s.camera, p)
+    assert st["pixels_processed"] == 2048 * 2048
+    assert st["samples_processed"] == 2048 * 2048 * 16
+    assert st["samples_processed"] + st["reflections"] == st["rays_processed"] + st["recursion_depth_hits"]
+    assert np.isfinite(img).all() and img.min() >= 0.0 and img.max() <= 1.0
+    for y in (0, 1024, 2047):  # one full row each, 2048 x 16 samples
+        ref, _ = O.render(s.view, s.camera, p, rows=(y, y + 1))
+        assert_bit_exact(img[y:y + 1], ref[y:y + 1])

@@ -1,0 +1,147 @@
+"""Pin the oracle (CPU restatement) to the reference's own unit-test answers.
+
+Each test restates one reference test (file:line in the name's docstring) with
+the committed fixtures of tests/golden/golden.json.  CPU only.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle_py as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+XORO, XOSHI = 0, 1
+
+
+def f32(x):
+    return np.float32(x)
+
+
+def test_prng_streams_match_python_emulation(golden):
+    """std.rand Xoroshiro128 / Xoshiro256 seeded by SplitMix64 (bit-exact)."""
+    S = golden["streams"]
+    for name, prng in (("xoroshiro128", XORO), ("xoshiro256", XOSHI)):
+        for seed in (0, 42, 0x123456789ABCDEF):
+            want = np.array([int(v) for v in S[f"{name}_u64_seed{seed}"]], dtype=np.uint64)
+            np.testing.assert_array_equal(O.prng_u64(prng, seed, 64), want)
+            wantf = np.array(S[f"{name}_f32_seed{seed}"], dtype=np.float32)
+            np.testing.assert_array_equal(O.prng_f32(prng, seed, 64), wantf)
+
+
+def test_counter_keys(golden):
+    for k in golden["streams"]["counter_keys_seed42"]:
+        want = np.array([int(v) for v in k["u64"]], dtype=np.uint64)
+        np.testing.assert_array_equal(O.prng_u64(XORO, int(k["key"]), 8), want)
+
+
+@pytest.mark.parametrize("which,name", [(0, "randomVector"), (1, "randomVectorInUnitSphere"),
+                                        (2, "randomUnitVector_old"), (3, "randomUnitVector")])
+def test_sample_golden_vectors(golden, which, name):
+    """sample.zig:70-118 with DefaultPrng.init(0): pins Xoroshiro128 as the generator."""
+    g = golden["reference_tests"]["sample"]
+    v = O.sample_vector(XORO, g["seed"], which)
+    assert np.all(np.abs(v - np.array(g[name], np.float32)) < g["tol"])
+    if which == 0:
+        assert np.linalg.norm(v) > 1.0
+    elif which == 1:
+        assert np.linalg.norm(v) < 1.0
+    else:
+        assert 0.99 < np.linalg.norm(v) < 1.01
+
+
+def test_sample_vectors_reject_xoshiro256(golden):
+    """The golden vectors of sample.zig do NOT come from Xoshiro256."""
+    g = golden["reference_tests"]["sample"]
+    v = O.sample_vector(XOSHI, g["seed"], 0)
+    assert not np.all(np.abs(v - np.array(g["randomVector"], np.float32)) < g["tol"])
+
+
+def test_ray_at(golden):
+    """ray.zig:32-39: Ray.init normalizes; rayAt(2) exact in f32."""
+    g = golden["reference_tests"]["ray_at"]
+    np.testing.assert_array_equal(O.ray_at(g["origin"], g["direction"], g["t"]),
+                                  np.array(g["expected"], np.float32))
+
+
+def test_unit_vector(golden):
+    """vector.zig:210-225 (zero vector -> NaN)."""
+    for case in golden["reference_tests"]["unit_vector"]:
+        np.testing.assert_array_equal(O.unit_vector(case["v"]), np.array(case["expected"], np.float32))
+    assert np.all(np.isnan(O.unit_vector([0, 0, 0])))
+
+
+def test_triangle_hit_and_miss(golden):
+    """triangle.zig:84-118."""
+    g = golden["reference_tests"]["triangle_miss"]
+    hit, _ = O.triangle_hit(g["a"], g["b"], g["c"], g["origin"], g["direction"], g["t_min"], g["t_max"])
+    assert not hit
+    g = golden["reference_tests"]["triangle_hit"]
+    hit, out = O.triangle_hit(g["a"], g["b"], g["c"], g["origin"], g["direction"], g["t_min"], g["t_max"])
+    assert hit
+    np.testing.assert_array_equal(out[0:3], np.array(g["location"], np.float32))
+    np.testing.assert_array_equal(out[3:6], np.array(g["normal"], np.float32))
+    assert out[6] == f32(g["t"])
+    assert bool(out[7]) == g["front_face"]
+
+
+def test_triangle_single_sided():
+    """det >= 1e-6 (triangle.zig:62): the same triangle seen from behind misses."""
+    a, b, c = [10, 5, 1], [-10, -10, 1], [-10, 10, 1]
+    hit, _ = O.triangle_hit(a, b, c, [0, 0, 10], [0, 0, -1], 0.1, 1e4)
+    assert not hit
+
+
+def test_aabb(golden):
+    """aabb.zig:151-254."""
+    R = golden["reference_tests"]
+    g = R["aabb_surface_area"]
+    assert O.aabb_surface_area(g["c1"], g["c2"]) == f32(g["expected"])
+    g = R["aabb_hit"]
+    for case in g["cases"]:
+        assert O.aabb_hit(g["c1"], g["c2"], g["origin"], case["direction"], g["t_min"], g["t_max"]) == case["hit"]
+
+
+def test_aabb_axes_tested_independently():
+    """aabb.zig:120-124 tests each axis against [t_min, t_max] alone: a ray that
+    passes beside a box (its x and y slab intervals do not overlap each other)
+    still "hits" it.  The GPU's reference traversal mode must reproduce this."""
+    # box [1,2]x[1,2]x[-1,1]; ray from origin along (1, 0.2, 0): the x-slab is
+    # entered at t=1..2, the y-slab at t=5..10: disjoint, yet accepted.
+    assert O.aabb_hit([1, 1, -1], [2, 2, 1], [0, 0, 0], [1, 0.2, 0], 0.001, np.inf)
+
+
+def _read_ppm(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(maxsplit=4)
+    w, h = int(parts[1]), int(parts[2])
+    raw = np.frombuffer(parts[4][: w * h * 3], dtype=np.uint8).reshape(h, w, 3)
+    return raw
+
+
+def test_texture_earthmap(golden):
+    """texture.zig:90-103: PNG decode + row flip + c/255 + nearest texel (exact)."""
+    g = golden["reference_tests"]["texture_earthmap"]
+    raw = _read_ppm(os.path.join(REPO, g["file"]))
+    img = (raw[::-1].astype(np.float32) / np.float32(255.0)).astype(np.float32)  # png_image.zig:86
+    for case in g["cases"]:
+        got = O.texture_albedo(img, g["u_offset"], g["v_offset"], *case["uv"])
+        np.testing.assert_array_equal(got, np.array(case["expected"], np.float32))
+
+
+def test_math_restatements_close_to_libm():
+    """sin/cos/acos/atan/atan2/pow restatements agree with libm to a few ulp
+    (they are not pinned bit-exactly to Zig: no Zig toolchain here)."""
+    x = np.linspace(0, 6.2831, 997, dtype=np.float32)
+    np.testing.assert_allclose(O.math1("sin", x), np.sin(x.astype(np.float64)), atol=3e-7)
+    np.testing.assert_allclose(O.math1("cos", x), np.cos(x.astype(np.float64)), atol=3e-7)
+    y = np.linspace(-1, 1, 1001, dtype=np.float32)
+    np.testing.assert_allclose(O.math1("acos", y), np.arccos(y.astype(np.float64)), rtol=3e-7, atol=3e-7)
+    np.testing.assert_allclose(O.math1("atan", y * 10), np.arctan(y.astype(np.float64) * 10), rtol=3e-7)
+    ys, xs = np.meshgrid(y[::50], y[::50])
+    got = O.math2("atan2", ys.ravel(), xs.ravel())
+    np.testing.assert_allclose(got, np.arctan2(ys.ravel().astype(np.float64), xs.ravel()), rtol=3e-7, atol=3e-7)
+    p = np.linspace(0, 2, 501, dtype=np.float32)
+    np.testing.assert_allclose(O.math2("pow", p, np.full_like(p, 5.0)), p.astype(np.float64) ** 5, rtol=1e-6)
+    assert O.math2("pow", [0.0], [5.0])[0] == 0.0 and O.math2("pow", [1.0], [5.0])[0] == 1.0

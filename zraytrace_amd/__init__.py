@@ -1,0 +1,199 @@
+"""zraytrace_amd — MI355X (gfx950) path of zraytrace's per-pixel sampling loop.
+
+Python host helpers over the C ABI (include/zrt.h, libzrt.so).  The reference
+names carry over: ``render`` replaces raytrace.render (raytrace.zig:136-203),
+``load_scene`` builds the scenes of scenes.zig:267-277 (through the C++ host
+mirror in csrc/scene_io.cpp), ``RenderParams`` mirrors raytrace.zig:102-108.
+
+There is no CPU fallback: every call that renders goes through the HIP kernel
+in libzrt.so and raises ZrtError(ZRT_E_NODEVICE) without an MI355X.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import (ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256, ZRT_RNG_COUNTER,  # noqa: F401
+                   ZRT_RNG_REFERENCE_STREAM, ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE,
+                   ZrtError, check)
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASSETS = os.path.join(REPO, "assets")
+
+SCENES = {0: "manAndBall", 1: "threeBalls", 2: "bunnyAndBall", 3: "teapotAndBall",
+          4: "teapotAndBallCircle", 5: "goat"}
+
+
+def lib():
+    return _ffi.load()
+
+
+@dataclass
+class RenderParams:
+    """raytrace.zig:102-108 plus the knobs of the GPU path."""
+    width: int
+    height: int
+    samples_per_pixel: int
+    max_depth: int
+    bounded_volume_hierarchy: bool = True
+    seed: int = 42
+    rng_mode: int = ZRT_RNG_COUNTER
+    prng: int = ZRT_PRNG_XOROSHIRO128
+    traversal: int = ZRT_TRAVERSAL_FAST
+    rank: int = 0
+    world_size: int = 1
+    device: int = 0
+
+    def abi(self) -> _ffi.Params:
+        p = _ffi.Params()
+        p.width, p.height = self.width, self.height
+        p.samples_per_pixel, p.max_depth = self.samples_per_pixel, self.max_depth
+        p.bounded_volume_hierarchy = 1 if self.bounded_volume_hierarchy else 0
+        p.rng_mode, p.prng, p.traversal = self.rng_mode, self.prng, self.traversal
+        p.seed = self.seed
+        p.rank, p.world_size, p.device = self.rank, self.world_size, self.device
+        p.flags = 0
+        return p
+
+
+class LoadedScene:
+    """A scene of scenes.zig built by the C++ host mirror (zrt_scene_load)."""
+
+    def __init__(self, index: int, assets_dir: str = ASSETS):
+        L = lib()
+        h = C.c_void_p()
+        cam = _ffi.Camera()
+        check(L.zrt_scene_load(index, assets_dir.encode(), C.byref(h), C.byref(cam)))
+        self._h = h
+        self.index = index
+        self.camera = cam
+        self.view = L.zrt_scene_view(h)  # POINTER(Scene)
+
+    @property
+    def n_prims(self) -> int:
+        return self.view.contents.n_prims
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().zrt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_scene(index: int, assets_dir: str = ASSETS) -> LoadedScene:
+    return LoadedScene(index, assets_dir)
+
+
+def camera_init(look_from, look_at, vup, vfov, aspect) -> _ffi.Camera:
+    """Camera.init (camera.zig:17-35)."""
+    f3 = C.c_float * 3
+    out = _ffi.Camera()
+    check(lib().zrt_camera_init(f3(*look_from), f3(*look_at), f3(*vup), vfov, aspect, C.byref(out)))
+    return out
+
+
+def render(scene, camera: _ffi.Camera, params: RenderParams):
+    """raytrace.render on the GPU: returns (image[H, W, 3] f32, row 0 = bottom; stats)."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+    st = _ffi.Stats()
+    p = params.abi()
+    check(lib().zrt_render(view, C.byref(camera), C.byref(p),
+                           out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+    return out, st.as_dict()
+
+
+class RenderContext:
+    """Device-resident scene (zrt_ctx_*): build + upload once, render many."""
+
+    def __init__(self, scene, params: RenderParams):
+        view = scene.view if isinstance(scene, LoadedScene) else scene
+        self._scene = scene  # keep the host arrays alive while the ctx exists
+        h = C.c_void_p()
+        p = params.abi()
+        check(lib().zrt_ctx_create(view, C.byref(p), C.byref(h)))
+        self._h = h
+
+    def tile_count(self, params: RenderParams) -> int:
+        n = C.c_uint32()
+        p = params.abi()
+        check(lib().zrt_ctx_tile_count(self._h, C.byref(p), C.byref(n)))
+        return n.value
+
+    def render_tiles(self, camera, params: RenderParams, dev_tiles: int, stream: int = 0):
+        p = params.abi()
+        check(lib().zrt_ctx_render_tiles(self._h, C.byref(camera), C.byref(p),
+                                         C.c_void_p(dev_tiles), C.c_void_p(stream or None)))
+
+    def assemble(self, params: RenderParams, dev_gathered: int, dev_frame: int, stream: int = 0):
+        p = params.abi()
+        check(lib().zrt_ctx_assemble(self._h, C.byref(p), C.c_void_p(dev_gathered),
+                                     C.c_void_p(dev_frame), C.c_void_p(stream or None)))
+
+    def stats(self) -> dict:
+        st = _ffi.Stats()
+        check(lib().zrt_ctx_stats(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def kernel_ms(self) -> float:
+        ms = C.c_double()
+        check(lib().zrt_ctx_last_kernel_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().zrt_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def bvh_build(scene):
+    """The product's BVH (zrt_bvh_build) as numpy arrays (mins, maxs, left, right, max_depth)."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    nodes = C.POINTER(_ffi.BvhNode)()
+    n = C.c_uint32()
+    depth = C.c_uint32()
+    check(lib().zrt_bvh_build(view, C.byref(nodes), C.byref(n), C.byref(depth)))
+    try:
+        return nodes_to_numpy(nodes, n.value) + (depth.value,)
+    finally:
+        lib().zrt_free(C.cast(nodes, C.c_void_p))
+
+
+def nodes_to_numpy(nodes, n):
+    dt = np.dtype([("min", "<f4", 3), ("left", "<i4"), ("max", "<f4", 3), ("right", "<i4")])
+    buf = np.ctypeslib.as_array(C.cast(nodes, C.POINTER(C.c_uint8)), shape=(n * 32,)).copy()
+    a = buf.view(dt)
+    return a["min"].copy(), a["max"].copy(), a["left"].copy(), a["right"].copy()
+
+
+def debug_math(fn: int, x, y=None, device: int = 0):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    yp = None
+    if y is not None:
+        y = np.ascontiguousarray(y, dtype=np.float32)
+        yp = y.ctypes.data_as(C.POINTER(C.c_float))
+    check(lib().zrt_debug_math(fn, x.ctypes.data_as(C.POINTER(C.c_float)), yp,
+                               out.ctypes.data_as(C.POINTER(C.c_float)), x.size, device))
+    return out
+
+
+def debug_rng(prng: int, key: int, n: int, device: int = 0):
+    out = np.empty(n, dtype=np.uint64)
+    check(lib().zrt_debug_rng(prng, key, out.ctypes.data_as(C.POINTER(C.c_uint64)), n, device))
+    return out

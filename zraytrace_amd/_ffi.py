@@ -1,0 +1,159 @@
+"""ctypes view of include/zrt.h (the C ABI of libzrt.so).
+
+The structures mirror the header field for field; `load()` opens the in-tree
+``zraytrace_amd/libzrt.so`` built by ``__graft_entry__.build()`` and fails
+loudly when it is missing: there is no Python or CPU fallback for the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzrt.so")
+
+# ---- status / enums (zrt.h) --------------------------------------------------
+ZRT_OK = 0
+ZRT_E_INVALID = -1
+ZRT_E_NOMEM = -2
+ZRT_E_HIP = -3
+ZRT_E_UNSUPPORTED = -4
+ZRT_E_NODEVICE = -5
+ZRT_E_IO = -6
+ZRT_E_PARSE = -7
+
+ZRT_PRIM_SPHERE, ZRT_PRIM_TRIANGLE = 0, 1
+ZRT_MAT_LAMBERTIAN, ZRT_MAT_METAL, ZRT_MAT_DIELECTRIC = 0, 1, 2
+ZRT_TEX_COLOR, ZRT_TEX_IMAGE = 0, 1
+ZRT_RNG_COUNTER, ZRT_RNG_REFERENCE_STREAM = 0, 1
+ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256 = 0, 1
+ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE = 0, 1
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("origin", Vec3), ("lower_left_corner", Vec3),
+                ("horizontal", Vec3), ("vertical", Vec3)]
+
+
+class Prim(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("material", C.c_uint32), ("center", Vec3),
+                ("radius", C.c_float), ("a", Vec3), ("b", Vec3), ("c", Vec3)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("texture", C.c_uint32),
+                ("index_of_refraction", C.c_float)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("image", C.c_uint32), ("color", Vec3),
+                ("u_offset", C.c_float), ("v_offset", C.c_float)]
+
+
+class Image(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32),
+                ("pixels", C.POINTER(C.c_float))]
+
+
+class Scene(C.Structure):
+    _fields_ = [("prims", C.POINTER(Prim)), ("n_prims", C.c_uint32),
+                ("n_materials", C.c_uint32), ("materials", C.POINTER(Material)),
+                ("textures", C.POINTER(Texture)), ("n_textures", C.c_uint32),
+                ("n_images", C.c_uint32), ("images", C.POINTER(Image))]
+
+
+class Params(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32),
+                ("bounded_volume_hierarchy", C.c_uint32), ("rng_mode", C.c_uint32),
+                ("prng", C.c_uint32), ("traversal", C.c_uint32), ("seed", C.c_uint64),
+                ("rank", C.c_uint32), ("world_size", C.c_uint32),
+                ("device", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("recursion_depth_hits", C.c_uint64), ("reflections", C.c_uint64),
+                ("background_hits", C.c_uint64), ("pixels_processed", C.c_uint64),
+                ("samples_processed", C.c_uint64), ("rays_processed", C.c_uint64),
+                ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("preprocess_ms", C.c_double), ("upload_ms", C.c_double),
+                ("render_ms", C.c_double), ("gather_ms", C.c_double),
+                ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),
+                ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class BvhNode(C.Structure):
+    _fields_ = [("min", Vec3), ("left", C.c_int32), ("max", Vec3), ("right", C.c_int32)]
+
+
+# Every symbol include/zrt.h declares: (name, restype, argtypes)
+_P = C.c_void_p
+SIGNATURES = [
+    ("zrt_render", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+                             C.POINTER(C.c_float), C.POINTER(Stats)]),
+    ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                  C.POINTER(C.c_float), C.c_float, C.c_float,
+                                  C.POINTER(Camera)]),
+    ("zrt_last_error", C.c_char_p, []),
+    ("zrt_abi_version", C.c_int, []),
+    ("zrt_build_info", C.c_char_p, []),
+    ("zrt_ctx_create", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(_P)]),
+    ("zrt_ctx_destroy", C.c_int, [_P]),
+    ("zrt_ctx_tile_count", C.c_int, [_P, C.POINTER(Params), C.POINTER(C.c_uint32)]),
+    ("zrt_ctx_render_tiles", C.c_int, [_P, C.POINTER(Camera), C.POINTER(Params), _P, _P]),
+    ("zrt_ctx_assemble", C.c_int, [_P, C.POINTER(Params), _P, _P, _P]),
+    ("zrt_ctx_stats", C.c_int, [_P, C.POINTER(Stats)]),
+    ("zrt_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
+    ("zrt_scene_load", C.c_int, [C.c_uint32, C.c_char_p, C.POINTER(_P), C.POINTER(Camera)]),
+    ("zrt_scene_view", C.POINTER(Scene), [_P]),
+    ("zrt_scene_free", None, [_P]),
+    ("zrt_obj_read", C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.POINTER(Prim)),
+                               C.POINTER(C.c_uint32)]),
+    ("zrt_free", None, [_P]),
+    ("zrt_bvh_build", C.c_int, [C.POINTER(Scene), C.POINTER(C.POINTER(BvhNode)),
+                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("zrt_debug_math", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                 C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
+    ("zrt_debug_rng", C.c_int, [C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64),
+                                C.c_uint32, C.c_uint32]),
+]
+
+_lib = None
+
+
+class ZrtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"zrt error {code}: {msg}")
+        self.code = code
+
+
+def load(path: str = LIB_PATH):
+    """Open libzrt.so (the HIP path).  Raises if it was not built."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()'); there is no fallback path")
+    lib = C.CDLL(path)
+    for name, restype, argtypes in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != ZRT_OK:
+        raise ZrtError(rc, (load().zrt_last_error() or b"").decode())
+    return rc

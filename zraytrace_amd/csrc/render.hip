@@ -1,0 +1,1255 @@
+// render.hip — the MI355X path of the reference's per-pixel sampling loop.
+//
+// Replaces raytrace.render (raytrace.zig:136-203) + rayColor (:62-100) and
+// everything they call per sample: Camera.getRay (camera.zig:46-52), BVH/AABB
+// traversal (bvh.zig:187-205, aabb.zig:109-127), Sphere.hit / Triangle.hit
+// (sphere.zig:31-71, triangle.zig:48-70), HitRecord.init (hit_record.zig:28-41),
+// Material.scatter (material.zig:43-129), Sample.randomUnitVector
+// (sample.zig:47-61), Texture.albedo (texture.zig:20-74).
+//
+// Kernel structure (gfx950, wave64):
+//   * persistent grid (CUs x resident blocks), 256-thread blocks;
+//   * each lane owns one pixel at a time and walks its samples in order, so
+//     the per-pixel f32 sum is accumulated exactly as raytrace.zig:172-179
+//     does; when a lane's path ends it immediately starts the next sample, and
+//     when its pixel is done the wave refills its finished lanes from a global
+//     work counter with ONE atomic per wave (__ballot + popcount + mbcnt rank);
+//   * the recursion `attenuation * rayColor(...)` is unrolled into an
+//     iterative loop; the attenuations are stacked per lane and multiplied in
+//     reverse at path end so the product keeps the recursion's association;
+//   * BVH traversal uses a per-lane stack in LDS laid out [depth][lane]
+//     (conflict-free: every lane of a wave hits a distinct bank);
+//   * RNG: one Xoroshiro128+ (or Xoshiro256++) stream per (pixel, sample),
+//     seeded through SplitMix64 exactly as DefaultPrng.init seeds.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bvh_build.hpp"
+#include "device_math.hpp"
+#include "zrt.hpp"
+
+namespace zrt {
+
+// ---------------------------------------------------------------------------
+// device data layout
+// ---------------------------------------------------------------------------
+// nodes: 2 x float4 per node {min.xyz, left}, {max.xyz, right}; child >= 0 is
+//   a node index, child < 0 a primitive slot ref -(2*slot + kind) - 1.
+// prims: 3 x float4 per slot (slots in DFS leaf order, or list order):
+//   triangle {a.xyz, e1.x} {e1.yz, e2.xy} {e2.z, n.xyz}  (n = e1 x e2)
+//   sphere   {center.xyz, radius} {0} {0}
+// shade: 1 x float4 per slot: triangle {unit normal.xyz, tag},
+//   sphere {1/radius, 0, 0, tag}; tag = material | kind << 31 (as u32 bits)
+struct alignas(16) DevMaterial {
+  float r, g, b, ior;          // texture color / index of refraction
+  float u_off, v_off;          // image texture offsets
+  uint32_t kind, tex_kind;     // ZRT_MAT_*, ZRT_TEX_*
+  uint32_t img_w, img_h, img_off, pad;  // image texture (img_off in texels)
+};
+
+struct KArgs {
+  const float4* __restrict__ nodes;
+  const float4* __restrict__ prims;
+  const float4* __restrict__ shade;
+  const DevMaterial* __restrict__ mats;
+  const float* __restrict__ texels;
+  float4* __restrict__ att;            // [max_depth][n_lanes]
+  float* __restrict__ out;             // this rank's tiles, tile-major, 64 px x RGB
+  uint32_t* __restrict__ work_counter;
+  unsigned long long* __restrict__ counters;  // 6 x u64
+  uint32_t* __restrict__ error_flag;
+  float org[3], llc[3], hor[3], ver[3];
+  float f_width, f_height, color_scale, pad0;
+  uint32_t width, height, xbound, spp, max_depth;
+  uint32_t tiles_x, rank, world, total_work;
+  uint32_t n_list, stack_depth, n_lanes;
+  unsigned long long seed_mix;
+};
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------
+// RNG: std.rand DefaultPrng restated per (pixel, sample)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+__device__ __forceinline__ uint64_t splitmix_next(uint64_t& s) {
+  s += 0x9e3779b97f4a7c15ULL;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+template <int PRNG>
+struct Rng;
+
+template <>
+struct Rng<ZRT_PRNG_XOROSHIRO128> {
+  uint64_t s0, s1;
+  __device__ __forceinline__ void init(uint64_t key) {
+    uint64_t g = key;
+    s0 = splitmix_next(g);
+    s1 = splitmix_next(g);
+  }
+  __device__ __forceinline__ uint64_t next() {  // Xoroshiro128+
+    const uint64_t a = s0;
+    uint64_t b = s1;
+    const uint64_t r = a + b;
+    b ^= a;
+    s0 = rotl64(a, 55) ^ b ^ (b << 14);
+    s1 = rotl64(b, 36);
+    return r;
+  }
+};
+
+template <>
+struct Rng<ZRT_PRNG_XOSHIRO256> {
+  uint64_t s[4];
+  __device__ __forceinline__ void init(uint64_t key) {
+    uint64_t g = key;
+    s[0] = splitmix_next(g);
+    s[1] = splitmix_next(g);
+    s[2] = splitmix_next(g);
+    s[3] = splitmix_next(g);
+  }
+  __device__ __forceinline__ uint64_t next() {  // Xoshiro256++
+    const uint64_t r = rotl64(s[0] + s[3], 23) + s[0];
+    const uint64_t t = s[1] << 17;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl64(s[3], 45);
+    return r;
+  }
+};
+
+// Random.float(f32) / Random.boolean()
+template <class R>
+__device__ __forceinline__ float rand_float(R& r) {
+  const uint32_t s = (uint32_t)r.next();
+  return __uint_as_float((0x7fu << 23) | (s >> 9)) - 1.0f;
+}
+template <class R>
+__device__ __forceinline__ bool rand_bool(R& r) {
+  return (r.next() & 1u) != 0;
+}
+
+// ---------------------------------------------------------------------------
+// small vector helpers (evaluation order as vector.zig)
+// ---------------------------------------------------------------------------
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 u, V3 v) {
+  return mk(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 scale(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 unit(V3 v) {  // vector.zig:88-92
+  const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
+  return mk(v.x / l, v.y / l, v.z / l);
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
+__device__ __forceinline__ V3 refract(V3 v, V3 n, float ratio) {  // vector.zig:132-137
+  const float cos_theta = dev::fmin_z(dot(neg(v), n), 1.0f);
+  const V3 perp = scale(add(v, scale(n, cos_theta)), ratio);
+  const V3 par = scale(n, -dev::sqrt_rn(__builtin_fabsf(1.0f - (perp.x * perp.x + perp.y * perp.y + perp.z * perp.z))));
+  return add(perp, par);
+}
+
+// ---------------------------------------------------------------------------
+// traversal
+// ---------------------------------------------------------------------------
+struct RayT {
+  float ox, oy, oz;
+  float ix, iy, iz;  // 1/d per axis (aabb.zig:112 computes it per test; same bits)
+  float dx, dy, dz;
+};
+
+// aabb.zig:109-127: each axis against [t_min, t_max] on its own.
+// FAST additionally narrows the interval across axes (with a 2^-16 relative
+// margin) and reports the entry distance for near-first ordering.
+template <bool FAST>
+__device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const RayT& r, float t_max,
+                                         float* entry) {
+  const float t_min = 0.001f;
+  float a0 = (lo.x - r.ox) * r.ix, a1 = (hi.x - r.ox) * r.ix;
+  float b0 = (lo.y - r.oy) * r.iy, b1 = (hi.y - r.oy) * r.iy;
+  float c0 = (lo.z - r.oz) * r.iz, c1 = (hi.z - r.oz) * r.iz;
+  if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
+  if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
+  if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
+  const float an = dev::fmax_z(a0, t_min), ax = dev::fmin_z(a1, t_max);
+  const float bn = dev::fmax_z(b0, t_min), bx = dev::fmin_z(b1, t_max);
+  const float cn = dev::fmax_z(c0, t_min), cx = dev::fmin_z(c1, t_max);
+  bool ok = (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) for every axis
+  if (FAST) {
+    const float en = dev::fmax_z(dev::fmax_z(an, bn), cn);
+    const float ex = dev::fmin_z(dev::fmin_z(ax, bx), cx);
+    ok = ok && !(en > ex * 1.0000153f);
+    *entry = en;
+  }
+  return ok;
+}
+
+// Triangle.hit (triangle.zig:48-70) for the candidate slot; accepts when the
+// reference would (det >= 1e-6, t_min < t < t_max, u,v >= 0, u+v <= 1), with
+// equal-t ties going to the lower slot (= earlier in the reference's DFS).
+template <bool TIE>
+__device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int slot, const RayT& r,
+                                         float& best_t, int& best) {
+  const float4 p0 = prims[3 * slot + 0];
+  const float4 p1 = prims[3 * slot + 1];
+  const float4 p2 = prims[3 * slot + 2];
+  const V3 n = mk(p2.y, p2.z, p2.w);
+  const V3 d = mk(r.dx, r.dy, r.dz);
+  const float det = -dot(d, n);
+  if (!(det >= 1e-6f)) return;
+  const float inv_det = 1.0f / det;
+  const V3 ao = mk(r.ox - p0.x, r.oy - p0.y, r.oz - p0.z);
+  const V3 dao = cross(ao, d);
+  const V3 e1 = mk(p0.w, p1.x, p1.y);
+  const V3 e2 = mk(p1.z, p1.w, p2.x);
+  const float u = dot(e2, dao) * inv_det;
+  const float v = -dot(e1, dao) * inv_det;
+  const float t = dot(ao, n) * inv_det;
+  const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
+  if (t > 0.001f && in_range && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
+    best_t = t;
+    best = slot;
+  }
+}
+
+// Sphere.hit (sphere.zig:31-41, 53-56): nearest root in (t_min, t_max).
+template <bool TIE>
+__device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT& r, float& best_t,
+                                            int& best) {
+  const V3 oc = mk(r.ox - c.x, r.oy - c.y, r.oz - c.z);
+  const V3 d = mk(r.dx, r.dy, r.dz);
+  const float half_b = dot(oc, d);
+  const float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - (c.w * c.w);
+  const float disc = half_b * half_b - cc;
+  if (disc < 0.0f) return;
+  const float root = dev::sqrt_rn(disc);
+  const float t1 = -half_b - root;
+  const float t = (t1 > 0.001f) ? t1 : (-half_b + root);
+  const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
+  if (t > 0.001f && in_range) {
+    best_t = t;
+    best = slot;
+  }
+}
+
+template <bool TIE>
+__device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int ref, const RayT& r,
+                                          float& best_t, int& best, uint32_t& c_prims) {
+  const int code = -ref - 1;
+  const int slot = code >> 1;
+  ++c_prims;
+  if (code & 1) tri_test<TIE>(prims, slot, r, best_t, best);
+  else sphere_test<TIE>(prims[3 * slot], slot, r, best_t, best);
+}
+
+__device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
+
+// Closest hit over the BVH.  FAST: near-first order with the narrowed slab
+// test; REFERENCE: left-first DFS with exactly bvh.zig:187-205's tests.
+template <bool FAST>
+__device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int* __restrict__ stk,
+                                             float& best_t, int& best, uint32_t& c_nodes,
+                                             uint32_t& c_prims) {
+  const int stride = kBlock;
+  uint32_t sp = 0;
+  const uint32_t cap = a.stack_depth;
+  if (FAST) {
+    float e;
+    float4 lo = a.nodes[0], hi = a.nodes[1];
+    ++c_nodes;
+    if (!box_test<true>(lo, hi, r, best_t * 1.0000153f, &e)) return;
+    int left = as_int(lo.w), right = as_int(hi.w);
+    for (;;) {
+      if (left < 0) {
+        prim_test<true>(a.prims, left, r, best_t, best, c_prims);
+        if (right != left) prim_test<true>(a.prims, right, r, best_t, best, c_prims);
+      } else {
+        const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
+        const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
+        c_nodes += 2;
+        const float tb = best_t * 1.0000153f;
+        float el, er;
+        const bool hl = box_test<true>(l0, l1, r, tb, &el);
+        const bool hr = box_test<true>(r0, r1, r, tb, &er);
+        if (hl && hr) {
+          const bool rfirst = er < el;
+          const int far_idx = rfirst ? left : right;
+          if (sp < cap) stk[sp * stride] = far_idx;
+          else atomicOr(a.error_flag, 1u);
+          ++sp;
+          left = rfirst ? as_int(r0.w) : as_int(l0.w);
+          right = rfirst ? as_int(r1.w) : as_int(l1.w);
+          continue;
+        }
+        if (hl) { left = as_int(l0.w); right = as_int(l1.w); continue; }
+        if (hr) { left = as_int(r0.w); right = as_int(r1.w); continue; }
+      }
+      // pop: re-test the node's own box against the (possibly shrunk) best_t
+      bool found = false;
+      while (sp > 0) {
+        --sp;
+        const int idx = sp < cap ? stk[sp * stride] : 0;
+        const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
+        ++c_nodes;
+        if (box_test<true>(p0, p1, r, best_t * 1.0000153f, &e)) {
+          left = as_int(p0.w);
+          right = as_int(p1.w);
+          found = true;
+          break;
+        }
+      }
+      if (!found) return;
+    }
+  } else {
+    stk[0] = 0;
+    sp = 1;
+    while (sp > 0) {
+      --sp;
+      const int idx = stk[sp * stride];
+      const float4 lo = a.nodes[2 * idx], hi = a.nodes[2 * idx + 1];
+      ++c_nodes;
+      float e;
+      if (!box_test<false>(lo, hi, r, best_t, &e)) continue;
+      const int left = as_int(lo.w), right = as_int(hi.w);
+      if (left < 0) {
+        prim_test<false>(a.prims, left, r, best_t, best, c_prims);
+        if (right != left) prim_test<false>(a.prims, right, r, best_t, best, c_prims);
+      } else {
+        if (sp + 2 <= cap) {
+          stk[sp * stride] = right;
+          stk[(sp + 1) * stride] = left;
+          sp += 2;
+        } else {
+          atomicOr(a.error_flag, 1u);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// shading
+// ---------------------------------------------------------------------------
+// @floatToInt(u64, f) then clamp(.., 0, n-1) as it executes on x86-64.
+__device__ __forceinline__ uint32_t texel_index(float f, uint32_t n) {
+  if (f >= 0.0f && f < 18446744073709551616.0f) {
+    const float lim = (float)(n - 1);
+    return f >= lim ? n - 1 : (uint32_t)f;
+  }
+  if (f < 0.0f && f > -1.0f) return 0;
+  return n - 1;
+}
+
+// texture.zig:20-74
+__device__ __forceinline__ V3 albedo(const DevMaterial& m, const float* __restrict__ texels, float u, float v) {
+  if (m.tex_kind == ZRT_TEX_COLOR) return mk(m.r, m.g, m.b);
+  const float uu_first = 1.0f - u + m.u_off;
+  float uu = uu_first;
+  if (uu_first > 1.0f) uu = uu_first - 1.0f;
+  else if (uu_first < 0.0f) uu = uu_first + 1.0f;
+  const float vv_first = v + m.v_off;
+  float vv = vv_first;
+  if (vv_first > 1.0f) vv = vv_first - 1.0f;
+  else if (uu_first < 0.0f) vv = vv_first + 1.0f;  // texture.zig:66 tests uu_first
+  const uint32_t x = texel_index(uu * (float)m.img_w, m.img_w);
+  const uint32_t y = texel_index(vv * (float)m.img_h, m.img_h);
+  const float* p = texels + 3ull * ((uint64_t)m.img_off + (uint64_t)y * m.img_w + x);
+  return mk(p[0], p[1], p[2]);
+}
+
+// raytrace.zig:53-58
+__device__ __forceinline__ V3 background(V3 d) {
+  const V3 u = unit(d);
+  const float t = 0.5f * (u.y + 1.0f);
+  const float w = 1.0f - t;
+  return mk(w + 0.5f * t, w + 0.7f * t, w + 1.0f * t);
+}
+
+
+// ---------------------------------------------------------------------------
+// per-wave counter reduction: one 64-bit atomic per wave per counter
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v) {
+  uint32_t lo = v, hi = 0;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t olo = __shfl_xor(lo, off);
+    const uint32_t ohi = __shfl_xor(hi, off);
+    const uint32_t nlo = lo + olo;
+    hi = hi + ohi + (nlo < lo ? 1u : 0u);
+    lo = nlo;
+  }
+  if (__lane_id() == 0 && (lo | hi)) atomicAdd(dst, ((unsigned long long)hi << 32) | lo);
+}
+
+// ---------------------------------------------------------------------------
+// the sampling loop
+// ---------------------------------------------------------------------------
+constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
+constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
+
+template <int MODE /*0 list, 1 BVH fast, 2 BVH reference*/, int PRNG>
+__global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
+  extern __shared__ int lds_stack[];
+  int* stk = lds_stack + threadIdx.x;
+  const int lane = (int)__lane_id();
+  const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+
+  bool need = true, done = false, in_sample = false;
+  uint32_t work = 0, px = 0, py = 0, sample = 0;
+  uint64_t offset = 0;
+  float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
+  V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+  uint32_t depth_left = 0, nb = 0;
+  Rng<PRNG> rng;
+  rng.init(0);
+  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_prims = 0;
+
+  for (;;) {
+    // ---- refill lanes whose pixel is finished: one atomic per wave
+    const bool want = need && !done;
+    const unsigned long long m = __ballot(want);
+    if (m) {
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(a.work_counter, (uint32_t)__popcll(m));
+      base = __shfl(base, leader);
+      if (want) {
+        work = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (work >= a.total_work) {
+          done = true;
+        } else {
+          // tile-major work: local tile lt of this rank = global tile lt*world + rank
+          const uint32_t lt = work >> 6, p = work & 63u;
+          const uint32_t t = lt * a.world + a.rank;
+          px = (t % a.tiles_x) * 8u + (p & 7u);
+          py = (t / a.tiles_x) * 8u + (p >> 3);
+          if (px < a.xbound && py < a.height) {
+            need = false;
+            sample = 0;
+            acc_r = acc_g = acc_b = 0.0f;
+            in_sample = false;
+            offset = (uint64_t)py * a.width + px;
+          } else {
+            float* o3 = a.out + 3ull * work;  // outside the rendered area: black
+            o3[0] = 0.0f;
+            o3[1] = 0.0f;
+            o3[2] = 0.0f;
+          }
+        }
+      }
+    }
+    if (__ballot(!done) == 0ull) break;
+    if (done || need) continue;
+
+    // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
+    if (!in_sample) {
+      rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
+      const float u = ((float)px + rand_float(rng) - 0.5f) / a.f_width;
+      const float v = ((float)py + rand_float(rng) - 0.5f) / a.f_height;
+      const V3 llc = mk(a.llc[0], a.llc[1], a.llc[2]);
+      const V3 hor = mk(a.hor[0], a.hor[1], a.hor[2]);
+      const V3 ver = mk(a.ver[0], a.ver[1], a.ver[2]);
+      o = mk(a.org[0], a.org[1], a.org[2]);
+      d = unit(sub(add(add(llc, scale(hor, u)), scale(ver, v)), o));
+      depth_left = a.max_depth;
+      nb = 0;
+      in_sample = true;
+    }
+
+    // ---- one rayColor step (raytrace.zig:62-100)
+    bool path_end = false, sky = false;
+    V3 L = mk(0.0f, 0.0f, 0.0f);
+    if (depth_left == 0) {
+      ++c_depth;
+      path_end = true;
+    } else {
+      ++c_rays;
+      RayT r;
+      r.ox = o.x; r.oy = o.y; r.oz = o.z;
+      r.dx = d.x; r.dy = d.y; r.dz = d.z;
+      r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+      float best_t = __builtin_inff();
+      int best = -1;
+      if (MODE == 0) {
+        for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order, t_max shrinking
+          const uint32_t tag = __float_as_uint(a.shade[i].w);
+          if (tag >> 31) tri_test<false>(a.prims, (int)i, r, best_t, best);
+          else sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
+          ++c_prims;
+        }
+      } else {
+        traverse_bvh<MODE == 1>(a, r, stk, best_t, best, c_nodes, c_prims);
+      }
+      if (best < 0) {
+        ++c_bg;
+        L = background(d);
+        path_end = true;
+        sky = true;
+      } else {
+        // ---- HitRecord.init (hit_record.zig:28-41)
+        const float4 sh = a.shade[best];
+        const uint32_t tag = __float_as_uint(sh.w);
+        const DevMaterial mat = a.mats[tag & 0x7fffffffu];
+        const bool need_uv = mat.kind != ZRT_MAT_DIELECTRIC && mat.tex_kind == ZRT_TEX_IMAGE;
+        const V3 loc = add(o, scale(d, best_t));
+        V3 outward;
+        float tu = 0.0f, tv = 0.0f;
+        if (tag >> 31) {
+          outward = mk(sh.x, sh.y, sh.z);  // face_unit_normal
+          if (need_uv) {  // barycentric (u, v), same arithmetic as the hit test
+            const float4 p0 = a.prims[3 * best + 0];
+            const float4 p1 = a.prims[3 * best + 1];
+            const float4 p2 = a.prims[3 * best + 2];
+            const V3 n = mk(p2.y, p2.z, p2.w);
+            const float det = -dot(d, n);
+            const float inv_det = 1.0f / det;
+            const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
+            const V3 dao = cross(ao, d);
+            tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
+            tv = -dot(mk(p0.w, p1.x, p1.y), dao) * inv_det;
+          }
+        } else {
+          const float4 c = a.prims[3 * best];
+          outward = scale(sub(loc, mk(c.x, c.y, c.z)), sh.x);  // (p - c) * (1/r)
+          if (need_uv) {  // sphere.zig:47-51
+            const float theta = dev::acos_z(-outward.y);
+            const float phi = dev::atan2_z(-outward.z, -outward.x) + kPi;
+            tu = phi / kTwoPi;
+            tv = theta / kPi;
+          }
+        }
+        bool front = true;
+        V3 normal = outward;
+        if (dot(d, outward) > 0.0f) {
+          normal = neg(outward);
+          front = false;
+        }
+        // ---- Material.scatter (material.zig:43-129)
+        bool absorbed = false;
+        V3 att = mk(1.0f, 1.0f, 1.0f), nd;
+        if (mat.kind == ZRT_MAT_LAMBERTIAN) {
+          const float r1 = rand_float(rng);
+          const float r2 = rand_float(rng);
+          const float rr = dev::sqrt_rn(1.0f - r1 * r1);
+          float sn, cs;
+          dev::sincos_z(kTwoPi * r2, &sn, &cs);
+          V3 hv = mk(cs * rr, sn * rr, r1);
+          if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
+          nd = unit(add(normal, hv));
+          att = albedo(mat, a.texels, tu, tv);
+        } else if (mat.kind == ZRT_MAT_METAL) {
+          nd = unit(reflect(unit(d), normal));
+          if (dot(nd, normal) > 0.0f) att = albedo(mat, a.texels, tu, tv);
+          else absorbed = true;
+        } else {
+          const float ratio = front ? (1.0f / mat.ior) : mat.ior;
+          const V3 ud = unit(d);
+          const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+          const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
+          bool refl = ratio * sin_theta > 1.0f;
+          if (!refl) {
+            const float r0 = (1.0f - ratio) / (1.0f + ratio);
+            const float reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+            refl = reflectance > rand_float(rng);
+          }
+          nd = unit(refl ? reflect(ud, normal) : refract(ud, normal, ratio));
+        }
+        if (absorbed) {
+          path_end = true;  // black
+        } else {
+          ++c_refl;
+          if (depth_left > 1) {  // an attenuation pushed at depth 1 is never read
+            a.att[(uint64_t)nb * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+            ++nb;
+          }
+          o = loc;
+          d = nd;
+          --depth_left;
+        }
+      }
+    }
+
+    if (path_end) {
+      // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
+      V3 col = L;
+      if (sky) {
+        for (uint32_t i = nb; i-- > 0;) {
+          const float4 at = a.att[(uint64_t)i * a.n_lanes + gl];
+          col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
+        }
+      }
+      acc_r += col.x;
+      acc_g += col.y;
+      acc_b += col.z;
+      in_sample = false;
+      if (++sample == a.spp) {
+        float* o3 = a.out + 3ull * work;
+        o3[0] = acc_r * a.color_scale;
+        o3[1] = acc_g * a.color_scale;
+        o3[2] = acc_b * a.color_scale;
+        need = true;
+      }
+    }
+  }
+
+  wave_add_u64(&a.counters[0], c_depth);
+  wave_add_u64(&a.counters[1], c_refl);
+  wave_add_u64(&a.counters[2], c_bg);
+  wave_add_u64(&a.counters[3], c_rays);
+  wave_add_u64(&a.counters[4], c_nodes);
+  wave_add_u64(&a.counters[5], c_prims);
+}
+
+// Scatter gathered rank tiles into the framebuffer (raytrace.zig:182 layout).
+__global__ void assemble_kernel(const float* __restrict__ gathered, float* __restrict__ frame,
+                                const uint32_t* __restrict__ rank_base, uint32_t world,
+                                uint32_t tiles_x, uint32_t xbound, uint32_t height, uint32_t width,
+                                uint32_t total) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  // find the rank owning gathered pixel i (world is small)
+  uint32_t r = 0;
+  while (r + 1 < world && rank_base[r + 1] <= i) ++r;
+  const uint32_t w = i - rank_base[r];
+  const uint32_t lt = w >> 6, p = w & 63u;
+  const uint32_t t = lt * world + r;
+  const uint32_t px = (t % tiles_x) * 8u + (p & 7u);
+  const uint32_t py = (t / tiles_x) * 8u + (p >> 3);
+  if (px >= xbound || py >= height) return;
+  const size_t o = ((size_t)py * width + px) * 3;
+  frame[o + 0] = gathered[3ull * i + 0];
+  frame[o + 1] = gathered[3ull * i + 1];
+  frame[o + 2] = gathered[3ull * i + 2];
+}
+
+// Device evaluation of the path's math (parity probes against the oracle).
+__global__ void debug_math_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
+                                  float* __restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = x[i], b = y ? y[i] : 0.0f;
+  float s, c, r;
+  switch (fn) {
+    case 0: dev::sincos_z(a, &s, &c); r = s; break;
+    case 1: dev::sincos_z(a, &s, &c); r = c; break;
+    case 2: r = dev::acos_z(a); break;
+    case 3: r = dev::atan_z(a); break;
+    case 4: r = dev::sqrt_rn(a); break;
+    case 5: r = dev::atan2_z(a, b); break;
+    case 6: r = dev::pow5_z(a); break;
+    default: r = a / b; break;
+  }
+  out[i] = r;
+}
+
+template <int PRNG>
+__global__ void debug_rng_kernel(uint64_t key, unsigned long long* out, uint32_t n) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  Rng<PRNG> r;
+  r.init(key);
+  for (uint32_t i = 0; i < n; ++i) out[i] = r.next();
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+namespace {
+
+struct HipError {
+  hipError_t err;
+  std::string where;
+};
+
+#define HIPCHK(expr)                                                       \
+  do {                                                                     \
+    const hipError_t e_ = (expr);                                          \
+    if (e_ != hipSuccess) throw ::zrt::HipError{e_, std::string(#expr)};          \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  void alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+  }
+  void upload(const std::vector<T>& v) {
+    alloc(v.size());
+    if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int check_device(int dev) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+    return fail(ZRT_E_NODEVICE, "no HIP device visible (the HIP path needs an MI355X / gfx950)");
+  if (dev < 0 || dev >= count) return fail(ZRT_E_NODEVICE, "device ordinal out of range");
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(ZRT_E_NODEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(ZRT_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", libzrt is built for gfx950 only");
+  return ZRT_OK;
+}
+
+int validate_scene(const zrt_scene* s) {
+  if (!s) return fail(ZRT_E_INVALID, "scene is null");
+  if (s->n_prims && !s->prims) return fail(ZRT_E_INVALID, "prims is null");
+  if (s->n_prims >= (1u << 29)) return fail(ZRT_E_UNSUPPORTED, "more than 2^29 primitives");
+  for (uint32_t i = 0; i < s->n_prims; ++i) {
+    const zrt_prim& p = s->prims[i];
+    if (p.kind != ZRT_PRIM_SPHERE && p.kind != ZRT_PRIM_TRIANGLE) return fail(ZRT_E_INVALID, "unknown primitive kind");
+    if (p.material >= s->n_materials) return fail(ZRT_E_INVALID, "material index out of range");
+  }
+  for (uint32_t i = 0; i < s->n_materials; ++i) {
+    const zrt_material& m = s->materials[i];
+    if (m.kind > ZRT_MAT_DIELECTRIC) return fail(ZRT_E_INVALID, "unknown material kind");
+    if (m.kind != ZRT_MAT_DIELECTRIC) {
+      if (m.texture >= s->n_textures) return fail(ZRT_E_INVALID, "texture index out of range");
+      const zrt_texture& t = s->textures[m.texture];
+      if (t.kind > ZRT_TEX_IMAGE) return fail(ZRT_E_INVALID, "unknown texture kind");
+      if (t.kind == ZRT_TEX_IMAGE) {
+        if (t.image >= s->n_images) return fail(ZRT_E_INVALID, "image index out of range");
+        const zrt_image& im = s->images[t.image];
+        if (!im.pixels || im.width == 0 || im.height == 0) return fail(ZRT_E_INVALID, "empty image");
+      }
+    }
+  }
+  return ZRT_OK;
+}
+
+int validate_params(const zrt_params* p) {
+  if (!p) return fail(ZRT_E_INVALID, "params is null");
+  if (p->width == 0 || p->height == 0 || p->samples_per_pixel == 0)
+    return fail(ZRT_E_INVALID, "width, height and samples_per_pixel must be > 0");
+  if (p->width > 65535 || p->height > 65535 || p->samples_per_pixel > 65535 || p->max_depth > 65535)
+    return fail(ZRT_E_INVALID, "RenderParams fields are u16 (raytrace.zig:102-108)");
+  if (p->height > p->width)
+    return fail(ZRT_E_INVALID,
+                "height > width: raytrace.zig:168 iterates x over image.height and would write past the image");
+  if (p->rng_mode != ZRT_RNG_COUNTER)
+    return fail(ZRT_E_UNSUPPORTED,
+                "the single sequential reference stream cannot be split across GPU lanes; use ZRT_RNG_COUNTER");
+  if (p->prng > ZRT_PRNG_XOSHIRO256) return fail(ZRT_E_INVALID, "unknown prng");
+  if (p->traversal > ZRT_TRAVERSAL_REFERENCE) return fail(ZRT_E_INVALID, "unknown traversal");
+  if (p->world_size == 0 || p->rank >= p->world_size) return fail(ZRT_E_INVALID, "rank must be < world_size");
+  return ZRT_OK;
+}
+
+struct Geometry {
+  uint32_t xbound, tiles_x, tiles_y, n_tiles;
+};
+Geometry geometry(const zrt_params* p) {
+  Geometry g;
+  g.xbound = p->height;  // raytrace.zig:168: `while (x < image.height)`
+  g.tiles_x = (g.xbound + 7) / 8;
+  g.tiles_y = (p->height + 7) / 8;
+  g.n_tiles = g.tiles_x * g.tiles_y;
+  return g;
+}
+uint32_t rank_tiles(const Geometry& g, uint32_t rank, uint32_t world) {
+  return g.n_tiles > rank ? (g.n_tiles - rank + world - 1) / world : 0;
+}
+
+}  // namespace
+}  // namespace zrt
+
+struct zrt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool use_bvh = false;
+  uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
+  zrt::DevBuf<float4> nodes, prims, shade;
+  zrt::DevBuf<zrt::DevMaterial> mats;
+  zrt::DevBuf<float> texels;
+  zrt::DevBuf<float4> att;
+  zrt::DevBuf<unsigned long long> scratch;  // [0..5] counters, [6] work counter, [7] error
+  zrt::DevBuf<uint32_t> rank_base;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double preprocess_ms = 0, upload_ms = 0;
+  // last launch
+  uint32_t last_pixels = 0, last_spp = 0, launched = 0;
+  int cu_count = 0;
+  ~zrt_ctx() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace zrt {
+namespace {
+
+// Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
+void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
+  const double t0 = now_ms();
+  const uint32_t n = s->n_prims;
+  std::vector<uint32_t> slot_to_prim;
+  std::vector<float4> nodes;
+  uint32_t depth = 0;
+  if (use_bvh) {
+    const BuiltBvh bvh = build_bvh(s->prims, n);
+    depth = bvh.max_depth;
+    nodes.resize(2 * bvh.nodes.size());
+    std::vector<int32_t> prim_slot(n, -1);
+    auto ref_of = [&](int32_t child) -> int32_t {
+      if (child >= 0) return child;
+      const uint32_t prim = uint32_t(-child - 1);
+      if (prim_slot[prim] < 0) {
+        prim_slot[prim] = int32_t(slot_to_prim.size());
+        slot_to_prim.push_back(prim);
+      }
+      const int32_t kind = s->prims[prim].kind == ZRT_PRIM_TRIANGLE ? 1 : 0;
+      return -(2 * prim_slot[prim] + kind) - 1;
+    };
+    for (size_t i = 0; i < bvh.nodes.size(); ++i) {  // pre-order == reference DFS order
+      const BuildNode& b = bvh.nodes[i];
+      const int32_t l = ref_of(b.left);
+      const int32_t r = ref_of(b.right);
+      float4 lo, hi;
+      lo.x = b.mn[0]; lo.y = b.mn[1]; lo.z = b.mn[2];
+      hi.x = b.mx[0]; hi.y = b.mx[1]; hi.z = b.mx[2];
+      std::memcpy(&lo.w, &l, 4);
+      std::memcpy(&hi.w, &r, 4);
+      nodes[2 * i] = lo;
+      nodes[2 * i + 1] = hi;
+    }
+    c->n_nodes = uint32_t(bvh.nodes.size());
+  } else {
+    for (uint32_t i = 0; i < n; ++i) slot_to_prim.push_back(i);
+  }
+  std::vector<float4> prims(3 * size_t(slot_to_prim.size()));
+  std::vector<float4> shade(slot_to_prim.size());
+  for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
+    const zrt_prim& p = s->prims[slot_to_prim[sl]];
+    float4* q = &prims[3 * sl];
+    float4& sh = shade[sl];
+    uint32_t tag = p.material;
+    if (p.kind == ZRT_PRIM_TRIANGLE) {
+      // triangle.zig:35-38: e1 = b-a, e2 = c-a, n = e1 x e2, unit n = n / |n|
+      const float e1x = p.b.x - p.a.x, e1y = p.b.y - p.a.y, e1z = p.b.z - p.a.z;
+      const float e2x = p.c.x - p.a.x, e2y = p.c.y - p.a.y, e2z = p.c.z - p.a.z;
+      const float nx = e1y * e2z - e1z * e2y;
+      const float ny = e1z * e2x - e1x * e2z;
+      const float nz = e1x * e2y - e1y * e2x;
+      const float len = std::sqrt(nx * nx + ny * ny + nz * nz);
+      q[0] = make_float4(p.a.x, p.a.y, p.a.z, e1x);
+      q[1] = make_float4(e1y, e1z, e2x, e2y);
+      q[2] = make_float4(e2z, nx, ny, nz);
+      tag |= 0x80000000u;
+      sh = make_float4(nx / len, ny / len, nz / len, 0.0f);
+    } else {
+      q[0] = make_float4(p.center.x, p.center.y, p.center.z, p.radius);
+      q[1] = make_float4(0, 0, 0, 0);
+      q[2] = make_float4(0, 0, 0, 0);
+      sh = make_float4(1.0f / p.radius, 0.0f, 0.0f, 0.0f);  // sphere.zig:46 scale(1.0/radius)
+    }
+    std::memcpy(&sh.w, &tag, 4);
+  }
+  // materials + textures
+  std::vector<DevMaterial> mats(s->n_materials);
+  std::vector<uint64_t> img_off(s->n_images);
+  uint64_t texel_count = 0;
+  for (uint32_t i = 0; i < s->n_images; ++i) {
+    img_off[i] = texel_count;
+    texel_count += uint64_t(s->images[i].width) * s->images[i].height;
+  }
+  if (texel_count >= (1ull << 32)) throw Error(ZRT_E_UNSUPPORTED, "more than 2^32 texels");
+  for (uint32_t i = 0; i < s->n_materials; ++i) {
+    const zrt_material& m = s->materials[i];
+    DevMaterial dm{};
+    dm.kind = m.kind;
+    dm.ior = m.index_of_refraction;
+    dm.tex_kind = ZRT_TEX_COLOR;
+    if (m.kind != ZRT_MAT_DIELECTRIC) {
+      const zrt_texture& t = s->textures[m.texture];
+      dm.tex_kind = t.kind;
+      dm.r = t.color.x;
+      dm.g = t.color.y;
+      dm.b = t.color.z;
+      dm.u_off = t.u_offset;
+      dm.v_off = t.v_offset;
+      if (t.kind == ZRT_TEX_IMAGE) {
+        dm.img_w = s->images[t.image].width;
+        dm.img_h = s->images[t.image].height;
+        dm.img_off = uint32_t(img_off[t.image]);
+      }
+    }
+    mats[i] = dm;
+  }
+  std::vector<float> tex(3 * texel_count);
+  for (uint32_t i = 0; i < s->n_images; ++i)
+    std::memcpy(&tex[3 * img_off[i]], s->images[i].pixels,
+                sizeof(float) * 3 * size_t(s->images[i].width) * s->images[i].height);
+  const double t1 = now_ms();
+  c->nodes.upload(nodes);
+  c->prims.upload(prims);
+  c->shade.upload(shade);
+  c->mats.upload(mats);
+  c->texels.upload(tex);
+  c->preprocess_ms = t1 - t0;
+  c->upload_ms = now_ms() - t1;
+  c->use_bvh = use_bvh;
+  c->n_prims = n;
+  c->bvh_depth = depth;
+  c->stack_depth = use_bvh ? depth + 2 : 0;
+}
+
+template <int MODE, int PRNG>
+void* kernel_ptr() {
+  return reinterpret_cast<void*>(&render_kernel<MODE, PRNG>);
+}
+
+void* select_kernel(int mode, uint32_t prng) {
+  if (prng == ZRT_PRNG_XOSHIRO256) {
+    if (mode == 0) return kernel_ptr<0, ZRT_PRNG_XOSHIRO256>();
+    if (mode == 1) return kernel_ptr<1, ZRT_PRNG_XOSHIRO256>();
+    return kernel_ptr<2, ZRT_PRNG_XOSHIRO256>();
+  }
+  if (mode == 0) return kernel_ptr<0, ZRT_PRNG_XOROSHIRO128>();
+  if (mode == 1) return kernel_ptr<1, ZRT_PRNG_XOROSHIRO128>();
+  return kernel_ptr<2, ZRT_PRNG_XOROSHIRO128>();
+}
+
+int hip_fail(const HipError& e) {
+  return fail(ZRT_E_HIP, e.where + ": " + hipGetErrorString(e.err));
+}
+
+}  // namespace
+}  // namespace zrt
+
+using zrt::fail;
+
+extern "C" {
+
+int zrt_abi_version(void) { return ZRT_ABI_VERSION; }
+
+const char* zrt_build_info(void) {
+  return "libzrt: HIP path for gfx950 (MI355X); persistent wave64 path-tracing kernel; -ffp-contract=off";
+}
+
+int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** out) {
+  if (!out) return fail(ZRT_E_INVALID, "out is null");
+  *out = nullptr;
+  int rc = zrt::validate_scene(scene);
+  if (rc) return rc;
+  if (!params) return fail(ZRT_E_INVALID, "params is null");
+  rc = zrt::check_device(int(params->device));
+  if (rc) return rc;
+  std::unique_ptr<zrt_ctx> c(new zrt_ctx);
+  try {
+    c->device = int(params->device);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, c->device));
+    c->cu_count = prop.multiProcessorCount;
+    // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces
+    const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
+    zrt::build_device_scene(c.get(), scene, use_bvh);
+    c->scratch.alloc(8);
+    *out = c.release();
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  } catch (const zrt::Error& e) {
+    return fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(ZRT_E_NOMEM, "OutOfMemory");
+  }
+}
+
+int zrt_ctx_destroy(zrt_ctx* ctx) {
+  if (!ctx) return ZRT_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  delete ctx;
+  return ZRT_OK;
+}
+
+int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n_tiles) {
+  if (!ctx || !n_tiles) return fail(ZRT_E_INVALID, "null argument");
+  const int rc = zrt::validate_params(params);
+  if (rc) return rc;
+  *n_tiles = zrt::rank_tiles(zrt::geometry(params), params->rank, params->world_size);
+  return ZRT_OK;
+}
+
+int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p, float* dev_tiles,
+                         void* hip_stream) {
+  if (!c || !cam || !dev_tiles) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::validate_params(p);
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    const zrt::Geometry g = zrt::geometry(p);
+    const uint32_t my_tiles = zrt::rank_tiles(g, p->rank, p->world_size);
+    const int mode = !c->use_bvh ? 0 : (p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2 : 1);
+    void* kfn = zrt::select_kernel(mode, p->prng);
+    const size_t lds = size_t(c->stack_depth) * zrt::kBlock * sizeof(int);
+    int per_cu = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
+    per_cu = std::max(1, std::min(per_cu, 8));
+    uint32_t grid = uint32_t(c->cu_count) * uint32_t(per_cu);
+    const uint32_t work = my_tiles * 64u;
+    grid = std::max(1u, std::min(grid, (work + zrt::kBlock - 1) / zrt::kBlock));
+    const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
+    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth) * n_lanes;
+    if (att_need * sizeof(float4) > (16ull << 30))
+      return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
+    if (c->att.n < att_need) c->att.alloc(att_need);
+    HIPCHK(hipMemsetAsync(c->scratch.p, 0, 8 * sizeof(unsigned long long), st));
+
+    zrt::KArgs a{};
+    a.nodes = c->nodes.p;
+    a.prims = c->prims.p;
+    a.shade = c->shade.p;
+    a.mats = c->mats.p;
+    a.texels = c->texels.p;
+    a.att = c->att.p;
+    a.out = dev_tiles;
+    a.counters = c->scratch.p;
+    a.work_counter = reinterpret_cast<uint32_t*>(c->scratch.p + 6);
+    a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + 7);
+    const zrt_vec3* v[4] = {&cam->origin, &cam->lower_left_corner, &cam->horizontal, &cam->vertical};
+    float* dst[4] = {a.org, a.llc, a.hor, a.ver};
+    for (int k = 0; k < 4; ++k) {
+      dst[k][0] = v[k]->x;
+      dst[k][1] = v[k]->y;
+      dst[k][2] = v[k]->z;
+    }
+    a.f_width = float(p->width);
+    a.f_height = float(p->height);
+    a.color_scale = 1.0f / float(p->samples_per_pixel);  // raytrace.zig:157
+    a.width = p->width;
+    a.height = p->height;
+    a.xbound = g.xbound;
+    a.spp = p->samples_per_pixel;
+    a.max_depth = p->max_depth;
+    a.tiles_x = g.tiles_x;
+    a.rank = p->rank;
+    a.world = p->world_size;
+    a.total_work = work;
+    a.n_list = c->use_bvh ? 0 : c->n_prims;
+    a.stack_depth = c->stack_depth;
+    a.n_lanes = uint32_t(n_lanes);
+    a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
+
+    HIPCHK(hipEventRecord(c->ev0, st));
+    if (work > 0) {
+      void* args[] = {&a};
+      HIPCHK(hipLaunchKernel(kfn, dim3(grid), dim3(zrt::kBlock), args, lds, st));
+    }
+    HIPCHK(hipEventRecord(c->ev1, st));
+    // count the pixels this rank renders (for samples/pixels counters)
+    uint64_t pixels = 0;
+    for (uint32_t lt = 0; lt < my_tiles; ++lt) {
+      const uint32_t t = lt * p->world_size + p->rank;
+      const uint32_t tx = t % g.tiles_x, ty = t / g.tiles_x;
+      const uint32_t w = std::min(8u, g.xbound - tx * 8u), h = std::min(8u, p->height - ty * 8u);
+      pixels += uint64_t(w) * h;
+    }
+    c->last_pixels = uint32_t(pixels);
+    c->last_spp = p->samples_per_pixel;
+    c->launched = 1;
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
+  if (!c || !out) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    unsigned long long h[8] = {0};
+    HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof(*out));
+    out->recursion_depth_hits = h[0];
+    out->reflections = h[1];
+    out->background_hits = h[2];
+    out->rays_processed = h[3];
+    out->node_visits = h[4];
+    out->prim_tests = h[5];
+    out->pixels_processed = c->last_pixels;
+    out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
+    out->preprocess_ms = c->preprocess_ms;
+    out->upload_ms = c->upload_ms;
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    out->render_ms = ms;
+    out->used_bvh = c->use_bvh ? 1 : 0;
+    out->bvh_nodes = c->n_nodes;
+    out->bvh_max_depth = c->bvh_depth;
+    out->n_gpus = 1;
+    if (h[7] != 0) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_last_kernel_ms(zrt_ctx* c, double* ms) {
+  if (!c || !ms) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    float f = 0.0f;
+    HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
+    *ms = f;
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_assemble(zrt_ctx* c, const zrt_params* p, const float* dev_gathered, float* dev_frame,
+                     void* hip_stream) {
+  if (!c || !dev_gathered || !dev_frame) return fail(ZRT_E_INVALID, "null argument");
+  const int rc = zrt::validate_params(p);
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    const zrt::Geometry g = zrt::geometry(p);
+    std::vector<uint32_t> base(p->world_size + 1, 0);
+    for (uint32_t r = 0; r < p->world_size; ++r) base[r + 1] = base[r] + zrt::rank_tiles(g, r, p->world_size) * 64u;
+    c->rank_base.upload(base);
+    const uint32_t total = base[p->world_size];
+    HIPCHK(hipMemsetAsync(dev_frame, 0, sizeof(float) * 3 * size_t(p->width) * p->height, st));
+    if (total) {
+      hipLaunchKernelGGL(zrt::assemble_kernel, dim3((total + 255) / 256), dim3(256), 0, st, dev_gathered,
+                         dev_frame, c->rank_base.p, p->world_size, g.tiles_x, g.xbound, p->height, p->width,
+                         total);
+      HIPCHK(hipGetLastError());
+    }
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
+               float* out_rgb, zrt_stats* stats) {
+  if (!camera || !out_rgb) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::validate_params(params);
+  if (rc) return rc;
+  zrt_params p = *params;
+  p.rank = 0;
+  p.world_size = 1;
+  zrt_ctx* c = nullptr;
+  rc = zrt_ctx_create(scene, &p, &c);
+  if (rc) return rc;
+  std::unique_ptr<zrt_ctx, int (*)(zrt_ctx*)> guard(c, zrt_ctx_destroy);
+  try {
+    uint32_t n_tiles = 0;
+    rc = zrt_ctx_tile_count(c, &p, &n_tiles);
+    if (rc) return rc;
+    zrt::DevBuf<float> tiles, frame;
+    tiles.alloc(size_t(n_tiles) * 64 * 3);
+    frame.alloc(size_t(p.width) * p.height * 3);
+    rc = zrt_ctx_render_tiles(c, camera, &p, tiles.p, nullptr);
+    if (rc) return rc;
+    rc = zrt_ctx_assemble(c, &p, tiles.p, frame.p, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(out_rgb, frame.p, sizeof(float) * 3 * size_t(p.width) * p.height, hipMemcpyDeviceToHost));
+    zrt_stats s;
+    rc = zrt_ctx_stats(c, &s);
+    if (rc) return rc;
+    if (stats) *stats = s;
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t n, uint32_t device) {
+  if (!x || !out) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::check_device(int(device));
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(int(device)));
+    zrt::DevBuf<float> dx, dy, dout;
+    dx.alloc(n);
+    dout.alloc(n);
+    HIPCHK(hipMemcpy(dx.p, x, n * sizeof(float), hipMemcpyHostToDevice));
+    if (y) {
+      dy.alloc(n);
+      HIPCHK(hipMemcpy(dy.p, y, n * sizeof(float), hipMemcpyHostToDevice));
+    }
+    hipLaunchKernelGGL(zrt::debug_math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, fn, dx.p,
+                       y ? dy.p : nullptr, dout.p, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, dout.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device) {
+  if (!out) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::check_device(int(device));
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(int(device)));
+    zrt::DevBuf<unsigned long long> d;
+    d.alloc(n);
+    if (prng == ZRT_PRNG_XOSHIRO256)
+      hipLaunchKernelGGL(zrt::debug_rng_kernel<ZRT_PRNG_XOSHIRO256>, dim3(1), dim3(64), 0, 0, key, d.p, n);
+    else
+      hipLaunchKernelGGL(zrt::debug_rng_kernel<ZRT_PRNG_XOROSHIRO128>, dim3(1), dim3(64), 0, 0, key, d.p, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, d.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,530 @@
+// scene_io.cpp — the caller side of the seam, restated in C++:
+//   scenes.zig (scene table), obj_reader.zig (OBJ -> triangles),
+//   png_image.zig:76-89 (texture rows flipped, c/255), camera.zig:17-35,
+// plus flattening of ArrayList(Surface) into the C-ABI arrays.
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+
+#include "zrt.hpp"
+
+namespace zrt {
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+const char* last_error_cstr() { return g_last_error.c_str(); }
+
+const Vec3 Vec3::origin{0.0f, 0.0f, 0.0f};
+const Vec3 Vec3::x_unit{1.0f, 0.0f, 0.0f};
+const Vec3 Vec3::y_unit{0.0f, 1.0f, 0.0f};
+const Vec3 Vec3::z_unit{0.0f, 0.0f, 1.0f};
+
+const Color Color::black{0.0f, 0.0f, 0.0f};
+const Color Color::white{1.0f, 1.0f, 1.0f};
+const Color Color::gold{1.0f, 0.843f, 0.0f};
+const Color Color::silver{0.752f, 0.752f, 0.752f};
+const Color Color::red{1.0f, 0.01f, 0.01f};
+const Color Color::green{0.01f, 1.0f, 0.01f};
+const Color Color::blue{0.01f, 0.01f, 1.0f};
+
+std::unique_ptr<Image> Image::init(uint32_t width, uint32_t height) {
+  auto img = std::make_unique<Image>();
+  img->width = width;
+  img->height = height;
+  img->pixels.assign(size_t(width) * height * 3, 0.0f);  // Image.init: all black
+  return img;
+}
+
+std::unique_ptr<Image> readImageFile(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw Error(ZRT_E_IO, "Can't open file " + path);
+  char magic[3] = {0, 0, 0};
+  unsigned w = 0, h = 0, maxv = 0;
+  if (std::fscanf(f, "%2s %u %u %u", magic, &w, &h, &maxv) != 4 || std::strcmp(magic, "P6") != 0 ||
+      maxv != 255 || w == 0 || h == 0) {
+    std::fclose(f);
+    throw Error(ZRT_E_IO, path + ": not an 8-bit P6 image (tools/prepare_assets.py writes them)");
+  }
+  std::fgetc(f);  // the single whitespace after maxval
+  std::vector<unsigned char> raw(size_t(w) * h * 3);
+  const size_t got = std::fread(raw.data(), 1, raw.size(), f);
+  std::fclose(f);
+  if (got != raw.size()) throw Error(ZRT_E_IO, path + ": truncated");
+  auto img = Image::init(w, h);
+  // png_image.zig:76-89: pixel (x, y) of the file lands at row (height - y - 1)
+  for (uint32_t y = 0; y < h; ++y) {
+    for (uint32_t x = 0; x < w; ++x) {
+      const unsigned char* px = &raw[(size_t(y) * w + x) * 3];
+      float* o = &img->pixels[((size_t(h) - y - 1) * w + x) * 3];
+      o[0] = float(px[0]) / 255.0f;
+      o[1] = float(px[1]) / 255.0f;
+      o[2] = float(px[2]) / 255.0f;
+    }
+  }
+  return img;
+}
+
+Texture Texture::initColor(Color c) {
+  Texture t;
+  t.kind = ZRT_TEX_COLOR;
+  t.color = c;
+  return t;
+}
+Texture Texture::initImage(const Image* img) { return initImageOpts(img, 0.19f, 0.1f); }
+Texture Texture::initImageOpts(const Image* img, float u_offset, float v_offset) {
+  Texture t;
+  t.kind = ZRT_TEX_IMAGE;
+  t.image = img;
+  t.u_offset = u_offset;
+  t.v_offset = v_offset;
+  return t;
+}
+
+Material Material::initLambertian(Random* random, Texture t) {
+  Material m;
+  m.kind = ZRT_MAT_LAMBERTIAN;
+  m.texture = t;
+  m.random = random;
+  return m;
+}
+Material Material::initMetal(Texture t) {
+  Material m;
+  m.kind = ZRT_MAT_METAL;
+  m.texture = t;
+  return m;
+}
+Material Material::initDielectric(Random* random, float ior) {
+  Material m;
+  m.kind = ZRT_MAT_DIELECTRIC;
+  m.index_of_refraction = ior;
+  m.random = random;
+  return m;
+}
+Material Material::greenMatte(Random* random) {
+  return initLambertian(random, Texture::initColor(Color::green));
+}
+const Material Material::black_metal = Material::initMetal(Texture::initColor(Color::black));
+const Material Material::silver_metal = Material::initMetal(Texture::initColor(Color::silver));
+const Material Material::blue_metal = Material::initMetal(Texture::initColor(Color::blue));
+const Material Material::green_metal = Material::initMetal(Texture::initColor(Color::green));
+
+Surface Surface::initSphere(Vec3 center, float radius, const Material* m) {
+  Surface s;
+  s.kind = ZRT_PRIM_SPHERE;
+  s.center = center;
+  s.radius = radius;
+  s.material = m;
+  return s;
+}
+Surface Surface::initTriangle(Vec3 a, Vec3 b, Vec3 c, const Material* m) {
+  Surface s;
+  s.kind = ZRT_PRIM_TRIANGLE;
+  s.a = a;
+  s.b = b;
+  s.c = c;
+  s.material = m;
+  return s;
+}
+
+// camera.zig:17-35 (tan via libm: Zig's std.math.tan restatement is unpinned)
+Camera Camera::init(Vec3 look_from, Vec3 look_at, Vec3 vup, float vfov, float aspect_ratio) {
+  auto unit = [](Vec3 v) {
+    const float l = std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    return Vec3{v.x / l, v.y / l, v.z / l};
+  };
+  auto cross = [](Vec3 u, Vec3 v) {
+    return Vec3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+  };
+  const float theta = float(M_PI) * vfov / 180.0f;
+  const float h = std::tan(theta / 2.0f);
+  const float viewport_height = 2.0f * h;
+  const float viewport_width = aspect_ratio * viewport_height;
+  const Vec3 w = unit(look_from.minus(look_at));
+  const Vec3 u = unit(cross(vup, w));
+  const Vec3 v = cross(w, u);
+  Camera c;
+  c.origin = look_from;
+  c.horizontal = u.scale(viewport_width);
+  c.vertical = v.scale(viewport_height);
+  c.lower_left_corner =
+      look_from.minus(c.horizontal.scale(1.0f / 2.0f)).minus(c.vertical.scale(1.0f / 2.0f)).minus(w);
+  if (std::isnan(w.x) || std::isnan(u.x)) throw Error(ZRT_E_INVALID, "Camera.init: degenerate basis");
+  return c;
+}
+
+zrt_camera Camera::abi() const {
+  zrt_camera o;
+  o.origin = {origin.x, origin.y, origin.z};
+  o.lower_left_corner = {lower_left_corner.x, lower_left_corner.y, lower_left_corner.z};
+  o.horizontal = {horizontal.x, horizontal.y, horizontal.z};
+  o.vertical = {vertical.x, vertical.y, vertical.z};
+  return o;
+}
+
+// ---- obj_reader.zig -------------------------------------------------------
+namespace {
+
+std::vector<std::string> tokenize(const std::string& s, char delim) {
+  // std.mem.tokenize: split on the delimiter, skipping empty tokens
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && s[i] == delim) ++i;
+    size_t j = i;
+    while (j < s.size() && s[j] != delim) ++j;
+    if (j > i) out.push_back(s.substr(i, j - i));
+    i = j;
+  }
+  return out;
+}
+
+float parse_f32(const std::string& tok, const std::string& where) {
+  if (tok.empty()) throw Error(ZRT_E_PARSE, where + ": missing coordinate");
+  errno = 0;
+  char* end = nullptr;
+  const float v = std::strtof(tok.c_str(), &end);
+  if (end != tok.c_str() + tok.size()) throw Error(ZRT_E_PARSE, where + ": bad float '" + tok + "'");
+  return v;
+}
+
+uint64_t parse_u64(const std::string& tok, const std::string& where) {
+  if (tok.empty() || tok[0] < '0' || tok[0] > '9')
+    throw Error(ZRT_E_PARSE, where + ": bad index '" + tok + "'");
+  char* end = nullptr;
+  errno = 0;
+  const unsigned long long v = std::strtoull(tok.c_str(), &end, 10);
+  if (end != tok.c_str() + tok.size() || errno == ERANGE)
+    throw Error(ZRT_E_PARSE, where + ": bad index '" + tok + "'");
+  return v;
+}
+
+}  // namespace
+
+std::vector<Surface> readObjFile(const std::string& path, const Material* material) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) throw Error(ZRT_E_IO, "Can't open file " + path);
+  std::vector<Vec3> vertexes;
+  std::vector<Surface> surfaces;
+  std::string line;
+  uint64_t lineno = 0;
+  while (std::getline(in, line)) {  // readUntilDelimiterAlloc(.., '\n', ..)
+    ++lineno;
+    if (line.size() > 20000) throw Error(ZRT_E_PARSE, path + ": line too long (StreamTooLong)");
+    if (line.empty()) continue;
+    if (line.back() == '\r') line.pop_back();
+    const std::string where = path + ":" + std::to_string(lineno);
+    if (line.size() >= 2 && line[0] == 'v' && line[1] == ' ') {
+      const auto tok = tokenize(line, ' ');
+      const float x = parse_f32(tok.size() > 1 ? tok[1] : "", where);
+      const float y = parse_f32(tok.size() > 2 ? tok[2] : "", where);
+      const float z = parse_f32(tok.size() > 3 ? tok[3] : "", where);
+      vertexes.push_back(Vec3{x, y, z});
+    } else if (line.size() >= 2 && line[0] == 'f' && line[1] == ' ') {
+      const auto tok = tokenize(line, ' ');
+      std::vector<uint64_t> fv;
+      for (size_t i = 1; i < tok.size(); ++i) {
+        // parseFaceVertex: only the vertex index is used downstream
+        const auto parts = tokenize(tok[i], '/');
+        fv.push_back(parse_u64(parts.empty() ? "" : parts[0], where));
+        for (size_t k = 1; k < parts.size() && k < 3; ++k) parse_u64(parts[k], where);
+      }
+      if (fv.size() < 3 || fv.size() > 6)
+        throw Error(ZRT_E_PARSE, where + ": WrongNumberOfFaceVertexes");
+      auto vert = [&](uint64_t idx) {
+        if (idx == 0 || idx > vertexes.size())
+          throw Error(ZRT_E_PARSE, where + ": vertex index out of range");
+        return vertexes[idx - 1];
+      };
+      // obj_reader.zig:66-111 fan order: 0,1,2 | 2,3,0 | 3,4,0 | 4,5,0
+      surfaces.push_back(Surface::initTriangle(vert(fv[0]), vert(fv[1]), vert(fv[2]), material));
+      if (fv.size() >= 4)
+        surfaces.push_back(Surface::initTriangle(vert(fv[2]), vert(fv[3]), vert(fv[0]), material));
+      if (fv.size() >= 5)
+        surfaces.push_back(Surface::initTriangle(vert(fv[3]), vert(fv[4]), vert(fv[0]), material));
+      if (fv.size() >= 6)
+        surfaces.push_back(Surface::initTriangle(vert(fv[4]), vert(fv[5]), vert(fv[0]), material));
+    } else if (line.size() >= 3 && line[0] == 'v' && line[1] == 'n' && line[2] == ' ') {
+      const auto tok = tokenize(line, ' ');
+      for (int k = 1; k <= 3; ++k) parse_f32(tok.size() > size_t(k) ? tok[k] : "", where);
+    }
+  }
+  return surfaces;
+}
+
+// ---- flattening -------------------------------------------------------------
+void FlatScene::finalize() {
+  view.prims = prims.data();
+  view.n_prims = uint32_t(prims.size());
+  view.materials = materials.data();
+  view.n_materials = uint32_t(materials.size());
+  view.textures = textures.data();
+  view.n_textures = uint32_t(textures.size());
+  view.images = images.data();
+  view.n_images = uint32_t(images.size());
+}
+
+FlatScene flatten(const std::vector<Surface>& surfaces) {
+  FlatScene fs;
+  std::map<const Material*, uint32_t> mat_index;
+  std::map<const Image*, uint32_t> img_index;
+  fs.prims.reserve(surfaces.size());
+  for (const Surface& s : surfaces) {
+    if (!s.material) throw Error(ZRT_E_INVALID, "surface without material");
+    auto it = mat_index.find(s.material);
+    uint32_t mi;
+    if (it == mat_index.end()) {
+      const Material& m = *s.material;
+      zrt_material zm{};
+      zm.kind = m.kind;
+      zm.index_of_refraction = m.index_of_refraction;
+      zm.texture = 0;
+      if (m.kind != ZRT_MAT_DIELECTRIC) {
+        zrt_texture zt{};
+        zt.kind = m.texture.kind;
+        zt.color = {m.texture.color.r, m.texture.color.g, m.texture.color.b};
+        zt.u_offset = m.texture.u_offset;
+        zt.v_offset = m.texture.v_offset;
+        if (m.texture.kind == ZRT_TEX_IMAGE) {
+          if (!m.texture.image) throw Error(ZRT_E_INVALID, "image texture without image");
+          auto ii = img_index.find(m.texture.image);
+          if (ii == img_index.end()) {
+            const Image* img = m.texture.image;
+            ii = img_index.emplace(img, uint32_t(fs.images.size())).first;
+            fs.images.push_back(zrt_image{img->width, img->height, img->pixels.data()});
+          }
+          zt.image = ii->second;
+        }
+        zm.texture = uint32_t(fs.textures.size());
+        fs.textures.push_back(zt);
+      }
+      mi = uint32_t(fs.materials.size());
+      fs.materials.push_back(zm);
+      mat_index.emplace(s.material, mi);
+    } else {
+      mi = it->second;
+    }
+    zrt_prim p{};
+    p.kind = s.kind;
+    p.material = mi;
+    p.center = {s.center.x, s.center.y, s.center.z};
+    p.radius = s.radius;
+    p.a = {s.a.x, s.a.y, s.a.z};
+    p.b = {s.b.x, s.b.y, s.b.z};
+    p.c = {s.c.x, s.c.y, s.c.z};
+    fs.prims.push_back(p);
+  }
+  fs.finalize();
+  return fs;
+}
+
+// ---- raytrace.render ----------------------------------------------------------
+std::unique_ptr<Image> render(Random* random, const Camera& camera,
+                              const std::vector<Surface>& surfaces, const RenderParams& params,
+                              zrt_stats* stats, uint32_t device) {
+  if (!random) throw Error(ZRT_E_INVALID, "render: random is null");
+  for (const Surface& s : surfaces)
+    if (s.material && s.material->random && s.material->random != random)
+      throw Error(ZRT_E_INVALID, "render: materials must share the render's *Random");
+  FlatScene fs = flatten(surfaces);
+  zrt_params p{};
+  p.width = params.width;
+  p.height = params.height;
+  p.samples_per_pixel = params.samples_per_pixel;
+  p.max_depth = params.max_depth;
+  p.bounded_volume_hierarchy = params.bounded_volume_hierarchy ? 1 : 0;
+  p.rng_mode = ZRT_RNG_COUNTER;
+  p.prng = ZRT_PRNG_XOROSHIRO128;
+  p.traversal = ZRT_TRAVERSAL_FAST;
+  p.seed = random->seed;
+  p.rank = 0;
+  p.world_size = 1;
+  p.device = device;
+  auto img = Image::init(params.width, params.height);
+  const zrt_camera cam = camera.abi();
+  const int rc = zrt_render(&fs.view, &cam, &p, img->pixels.data(), stats);
+  if (rc != ZRT_OK) throw Error(rc, zrt_last_error());
+  return img;
+}
+
+// ---- scenes.zig ------------------------------------------------------------------
+namespace {
+
+const Material* own(SceneData& sd, Material m) {
+  sd.materials.push_back(std::make_unique<Material>(m));
+  return sd.materials.back().get();
+}
+const Image* own_image(SceneData& sd, const std::string& path) {
+  sd.images.push_back(readImageFile(path));
+  return sd.images.back().get();
+}
+
+}  // namespace
+
+std::unique_ptr<SceneData> buildScene(uint32_t scene_index, const std::string& assets) {
+  auto sd = std::make_unique<SceneData>();
+  sd->prng = std::make_unique<DefaultPrng>(42);  // DefaultPrng.init(42) in every scene
+  Random* random = sd->prng->random();
+  auto& S = sd->surfaces;
+  const std::string dir = assets.empty() ? std::string(".") : assets;
+  auto mesh = [&](const char* file, const Material* m) {
+    for (const Surface& s : readObjFile(dir + "/" + file, m)) S.push_back(s);
+  };
+  switch (scene_index) {
+    case 0: {  // manAndBall (scenes.zig:26-52)
+      const float top = -2.33f, radius = 100.0f;
+      const Vec3 earth_center{1.66445508e-01f, top - radius, 7.37018966e+00f};
+      S.push_back(Surface::initSphere(earth_center, radius, own(*sd, Material::greenMatte(random))));
+      mesh("Man.obj", &Material::blue_metal);
+      sd->camera = Camera::init(Vec3{0.0f, 0.0f, -30.0f}, Vec3::z_unit, Vec3::y_unit, 45.0f, 1.0f);
+      break;
+    }
+    case 1: {  // threeBalls (scenes.zig:54-100)
+      const Image* earthmap = own_image(*sd, dir + "/earthmap.ppm");
+      const Image* nitor = own_image(*sd, dir + "/nitor-logo-25.ppm");
+      const Material* mirror = own(*sd, Material::initMetal(Texture::initColor(Color::silver)));
+      const Material* nitor_m = own(*sd, Material::initLambertian(random, Texture::initImage(nitor)));
+      const Material* green_matte = own(*sd, Material::greenMatte(random));
+      const Material* glass = own(*sd, Material::initDielectric(random, 1.52f));
+      const Material* earth = own(*sd, Material::initMetal(Texture::initImage(earthmap)));
+      S.push_back(Surface::initSphere(Vec3{1.0f, -102.5f, 4.0f}, 100.0f, green_matte));
+      S.push_back(Surface::initSphere(Vec3::z_unit.scale(8.0f), 2.0f, nitor_m));
+      S.push_back(Surface::initSphere(Vec3{-3.0f, -1.5f, 3.0f}, 1.0f, mirror));
+      S.push_back(Surface::initSphere(Vec3{3.0f, -1.0f, 4.0f}, 1.5f, earth));
+      S.push_back(Surface::initSphere(Vec3{-1.0f, -1.0f, 2.0f}, 0.7f, glass));
+      const Vec3 bubble{0.85f, -0.7f, 1.5f};
+      const float radius = 0.9f, thickness = 0.1f;  // comptime: -(0.9 - 0.1) = -0.8
+      S.push_back(Surface::initSphere(bubble, radius, glass));
+      S.push_back(Surface::initSphere(bubble, float(-(0.9 - 0.1)), glass));
+      (void)thickness;
+      sd->camera = Camera::init(Vec3{0.0f, 0.0f, -7.0f}, Vec3::z_unit, Vec3::y_unit, 45.0f, 1.0f);
+      break;
+    }
+    case 2: {  // bunnyAndBall (scenes.zig:102-128)
+      const float top = -0.33f, radius = 100.0f;
+      const Vec3 earth_center{1.66445508e-01f, top - radius, 7.37018966e+00f};
+      S.push_back(Surface::initSphere(earth_center, radius, own(*sd, Material::greenMatte(random))));
+      mesh("bunny.obj", &Material::silver_metal);
+      sd->camera = Camera::init(Vec3{0.0f, 0.0f, -0.5f}, Vec3::z_unit, Vec3::y_unit, 45.0f, 1.0f);
+      break;
+    }
+    case 3: {  // teapotAndBall (scenes.zig:206-232)
+      const float top = -2.33f, radius = 100.0f;
+      const Vec3 earth_center{1.66445508e-01f, top - radius, 7.37018966e+00f};
+      S.push_back(Surface::initSphere(earth_center, radius, own(*sd, Material::greenMatte(random))));
+      mesh("teapot.obj", &Material::blue_metal);
+      sd->camera = Camera::init(Vec3{0.0f, 0.0f, -10.0f}, Vec3::z_unit, Vec3::y_unit, 45.0f, 1.0f);
+      break;
+    }
+    case 4: {  // teapotAndBallCircle (scenes.zig:168-204)
+      const Image* earthmap = own_image(*sd, dir + "/earthmap.ppm");
+      const Material* purple = own(*sd, Material::initLambertian(random, Texture::initImage(earthmap)));
+      const float top = -2.33f, radius = 100.0f;
+      const Vec3 earth_center{1.66445508e-01f, top - radius, 7.37018966e+00f};
+      S.push_back(Surface::initSphere(Vec3::z_unit.scale(6.0f), -2.0f, &Material::silver_metal));
+      S.push_back(Surface::initSphere(Vec3{3.0f, -1.0f, 4.0f}, 1.0f, purple));
+      S.push_back(Surface::initSphere(earth_center, radius, own(*sd, Material::greenMatte(random))));
+      mesh("teapot.obj", &Material::blue_metal);
+      sd->camera = Camera::init(Vec3{-8.0f, 0.0f, -10.0f}, Vec3::z_unit, Vec3::y_unit, 45.0f, 1.0f);
+      break;
+    }
+    case 5:  // goat (scenes.zig:234-260)
+      throw Error(ZRT_E_IO,
+                  "scene 5 needs models/high_poly_goat.obj, which the reference does not ship "
+                  "(.MISSING_LARGE_BLOBS)");
+    default:
+      throw Error(ZRT_E_INVALID, "UnkownSceneIndex");  // scenes.zig:263-265
+  }
+  sd->flat = flatten(sd->surfaces);
+  return sd;
+}
+
+}  // namespace zrt
+
+// ---- C ABI: ingestion helpers ----------------------------------------------------
+struct zrt_scene_data {
+  std::unique_ptr<zrt::SceneData> sd;
+};
+
+extern "C" {
+
+const char* zrt_last_error(void) { return zrt::last_error_cstr(); }
+
+int zrt_camera_init(const float look_from[3], const float look_at[3], const float vup[3],
+                    float vfov_deg, float aspect_ratio, zrt_camera* out) {
+  if (!look_from || !look_at || !vup || !out) return zrt::fail(ZRT_E_INVALID, "null argument");
+  try {
+    const zrt::Camera c = zrt::Camera::init(zrt::Vec3{look_from[0], look_from[1], look_from[2]},
+                                            zrt::Vec3{look_at[0], look_at[1], look_at[2]},
+                                            zrt::Vec3{vup[0], vup[1], vup[2]}, vfov_deg, aspect_ratio);
+    *out = c.abi();
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  }
+}
+
+int zrt_scene_load(uint32_t scene_index, const char* assets_dir, zrt_scene_data** out,
+                   zrt_camera* camera) {
+  if (!out) return zrt::fail(ZRT_E_INVALID, "null out");
+  *out = nullptr;
+  try {
+    auto h = new zrt_scene_data;
+    h->sd = zrt::buildScene(scene_index, assets_dir ? assets_dir : "");
+    if (camera) *camera = h->sd->camera.abi();
+    *out = h;
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return zrt::fail(ZRT_E_NOMEM, "OutOfMemory");
+  }
+}
+
+const zrt_scene* zrt_scene_view(const zrt_scene_data* data) {
+  return data ? &data->sd->flat.view : nullptr;
+}
+
+void zrt_scene_free(zrt_scene_data* data) { delete data; }
+
+int zrt_obj_read(const char* path, uint32_t material, zrt_prim** out_prims, uint32_t* n_prims) {
+  if (!path || !out_prims || !n_prims) return zrt::fail(ZRT_E_INVALID, "null argument");
+  *out_prims = nullptr;
+  *n_prims = 0;
+  try {
+    static const zrt::Material dummy = zrt::Material::black_metal;
+    const auto tris = zrt::readObjFile(path, &dummy);
+    auto* p = static_cast<zrt_prim*>(std::malloc(sizeof(zrt_prim) * (tris.size() ? tris.size() : 1)));
+    if (!p) return zrt::fail(ZRT_E_NOMEM, "OutOfMemory");
+    for (size_t i = 0; i < tris.size(); ++i) {
+      zrt_prim q{};
+      q.kind = ZRT_PRIM_TRIANGLE;
+      q.material = material;
+      q.a = {tris[i].a.x, tris[i].a.y, tris[i].a.z};
+      q.b = {tris[i].b.x, tris[i].b.y, tris[i].b.z};
+      q.c = {tris[i].c.x, tris[i].c.y, tris[i].c.z};
+      p[i] = q;
+    }
+    *out_prims = p;
+    *n_prims = uint32_t(tris.size());
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  }
+}
+
+void zrt_free(void* p) { std::free(p); }
+
+}  // extern "C"
