@@ -139,6 +139,15 @@ def load(path: str = LIB_PATH):
     global _lib
     if _lib is not None and path == LIB_PATH:
         return _lib
+    # One HIP runtime per process: libzrt.so and torch both NEED
+    # libamdhip64.so.7, and torch ships its own copy (with its own HSA runtime).
+    # Whichever is loaded first is the one the process uses, and a second HSA
+    # runtime cannot open the GPU.  Load torch's first so device buffers, streams
+    # and RCCL (torch.distributed) share the runtime libzrt launches on.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build the HIP extension first "
