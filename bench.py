@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""bench.py — throughput of the HIP sampling loop on BASELINE.json's metric.
+
+Workload (BASELINE.json configs[3]): scene 2 of scenes.zig
+(bunny.obj + ground sphere, BVH), 2048x2048 pixels, 1024 samples per pixel,
+max depth 20, counter RNG seeded 42.  One step = one full frame: every rank
+renders its 8x8 tiles (tile t -> rank t % N) with the scene already resident
+in HBM, the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl")
+and assembled into the reference's framebuffer layout.  The frame is fixed as
+N grows: "scaling": "strong".
+
+value = rays of all ranks (raytrace.zig:69's rays_processed, counted on the
+device) / the max-over-ranks wall time of the timed steps, in Mrays/s.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mrays/s + achieved HBM GB/s, bunny BVH @ 2048², 1024spp, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(st, n_work_units, n_pixels):
+    """Bytes the sampling loop must touch per launch:
+    32 B per BVH node tested, 48 B per triangle test, 16 B per sphere test,
+    64 B per shaded hit (16 B shade record + 48 B material), 12 B per texel,
+    32 B per scatter (attenuation pushed + read back), 16 B per chunk sum
+    written and read, 12 B per output pixel."""
+    tri = st["prim_tests"] - st["sphere_tests"]
+    return (32 * st["node_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
+            + 12 * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of render_kernel measured by rocprofv3 PMC passes
+    (tools/gpu_profile.sh -> profiles/latest_pmc.json) for this exact config,
+    corrected as MI355X_MICROARCH.md §HBM prescribes; None if not measured."""
+    path = os.path.join(REPO, "profiles", "latest_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config") != config:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def cpu_baseline(scene, seconds_hint):
+    """The oracle (single-threaded C restatement, reference RNG stream) on a
+    bounded sample of the same scene: 128x128 @ 4 spp, depth 20."""
+    import zraytrace_amd as z
+    from oracle import oracle_py as O
+    w = h = 128
+    spp = 4
+    p = z.RenderParams(w, h, spp, 20, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
+    t0 = time.perf_counter()
+    _, st = O.render(scene.view, scene.camera, p)
+    dt = time.perf_counter() - t0
+    return {"value": st["rays_processed"] / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ (C restatement of the Zig path, reference RNG stream), scene 2 bunny, "
+                      f"{w}x{h} @ {spp} spp, depth 20: {st['rays_processed']} rays in {dt:.1f} s on 1 core "
+                      f"({os.cpu_count()} visible)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", type=int, default=2)
+    ap.add_argument("--width", type=int, default=2048)
+    ap.add_argument("--height", type=int, default=2048)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=20)
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--traversal", choices=["fast", "reference"], default="fast")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import zraytrace_amd as z
+    scene = z.load_scene(args.scene)
+    trav = z.ZRT_TRAVERSAL_FAST if args.traversal == "fast" else z.ZRT_TRAVERSAL_REFERENCE
+    params = z.RenderParams(args.width, args.height, args.spp, args.depth, traversal=trav,
+                            rank=rank, world_size=world, device=local, sample_chunk=args.chunk)
+    ctx = z.RenderContext(scene, params)
+    from zraytrace_amd.dist import gather_tiles, tile_counts
+    counts = tile_counts(params)
+    my_tiles, max_tiles = counts[rank], max(counts)
+    tiles = torch.zeros(max_tiles * 64 * 3, dtype=torch.float32, device="cuda")
+    frame = torch.empty(args.height * args.width * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
+    p0 = z.RenderParams(**{**params.__dict__, "rank": 0})
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        ctx.render_tiles(scene.camera, params, tiles.data_ptr(), stream)
+        kms = ctx.kernel_ms()  # HIP events around the kernel, on its launch stream
+        gathered = gather_tiles(tiles, counts, rank, world, dst=0)  # RCCL over xGMI
+        if rank == 0:
+            ctx.assemble(p0, gathered.data_ptr(), frame.data_ptr(), stream)
+        return kms
+
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        log(f"[rank {rank}] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f} s")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for i in range(args.steps):
+        kernel_ms.append(step())
+        log(f"[rank {rank}] step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = ctx.stats()  # counters of the last launch (identical every step: deterministic)
+    rays = torch.tensor([float(st["rays_processed"]), float(st["samples_processed"])], dtype=torch.float64,
+                        device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(rays, op=dist.ReduceOp.SUM)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    total_rays, total_samples = rays.tolist()
+    elapsed = el.item()
+
+    if rank == 0:
+        value = total_rays * args.steps / elapsed / 1e6
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        chunk = args.chunk or 64
+        n_units = my_tiles * 64 * ((args.spp + chunk - 1) // chunk)
+        algo = algorithmic_bytes(st, n_units, st["pixels_processed"])
+        achieved = algo / avg_kernel_s / 1e9
+        pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+                   "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
+        traffic, traffic_src = pmc_traffic(pmc_key)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: the reference's own scene 2 (models/bunny.obj + ground sphere), no dataset",
+            "config": {"workload": f"scene {args.scene} (bunnyAndBall) BVH, {args.width}x{args.height} @ "
+                                   f"{args.spp} spp, max depth {args.depth}",
+                       "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+                       "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk,
+                       "rng": "counter (Xoroshiro128+ per pixel-sample, seed 42)",
+                       "parallelism": f"image tiles 8x8 round-robin over {world} GPU(s) + RCCL gather"},
+            "rays_per_step": int(total_rays),
+            "samples_per_step": int(total_samples),
+            "rays_per_sample": round(total_rays / max(1.0, total_samples), 4),
+            "kernel_ms_avg": round(avg_kernel_s * 1e3, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_unit": "bytes per launch (rocprofv3 (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB)",
+                         "traffic_source": traffic_src,
+                         "kernel": "render_kernel<1,0> (BVH fast traversal)",
+                         "algorithmic_bytes_per_launch": int(algo),
+                         "per_ray": {"node_visits": round(st["node_visits"] / max(1, st["rays_processed"]), 2),
+                                     "prim_tests": round(st["prim_tests"] / max(1, st["rays_processed"]), 2),
+                                     "bytes": round(algo / max(1, st["rays_processed"]), 1)}},
+            "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("[rank 0] cpu baseline (oracle, 1 core) ...")
+            out["cpu_baseline"] = cpu_baseline(scene, 10)
+        print(json.dumps(out), flush=True)
+
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -146,7 +146,14 @@ typedef struct zrt_params {
   uint32_t rank;                     /* image-tile partition: this rank ... */
   uint32_t world_size;               /* ... of world_size (1 = whole frame) */
   uint32_t device;                   /* HIP device ordinal */
+  /* COUNTER mode: a pixel's samples are summed in chunks of sample_chunk
+   * consecutive samples (each chunk sequentially, as raytrace.zig:177 does),
+   * and the chunk sums are then added in chunk order.  0 selects 64.  With
+   * sample_chunk >= samples_per_pixel this is the reference's single
+   * sequential sum.  A chunk is the kernel's unit of work. */
+  uint32_t sample_chunk;
   uint32_t flags;                    /* reserved, 0 */
+  uint32_t reserved;
 } zrt_params;
 
 /* Progress counters (raytrace.zig:20-34) + timings. */
@@ -158,7 +165,10 @@ typedef struct zrt_stats {
   uint64_t samples_processed;
   uint64_t rays_processed;
   uint64_t node_visits;   /* BVH nodes whose box was tested (diagnostic) */
-  uint64_t prim_tests;    /* primitive intersection tests (diagnostic) */
+  uint64_t prim_tests;    /* primitive intersection tests, triangles + spheres */
+  uint64_t sphere_tests;  /* ... of which spheres */
+  uint64_t shade_fetches; /* closest hits shaded (hit record + material reads) */
+  uint64_t texel_fetches; /* image-texture lookups */
   double preprocess_ms;   /* BVH build + flatten (raytrace.zig:150) */
   double upload_ms;
   double render_ms;       /* kernel time (HIP events) */
@@ -200,7 +210,9 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
 int zrt_ctx_destroy(zrt_ctx* ctx);
 
 /* Number of 8x8 tiles this (rank, world_size) owns; its tile buffer holds
- * n_tiles*64*3 floats.  Tiles are dealt round-robin: tile t -> rank t % world. */
+ * n_tiles*64*3 floats.  Tiles are dealt round-robin: tile t -> rank t % world.
+ * Tiles cover x in [0, height) (raytrace.zig:168's bound) by y in [0, height).
+ * Host-only: ctx may be NULL. */
 int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n_tiles);
 
 /* Render this rank's tiles into dev_tiles (device pointer, tile-major,

@@ -620,11 +620,13 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
   const float f_width = (float)p->width;
   const float f_height = (float)p->height;
   const float color_scale = 1.0f / (float)p->samples_per_pixel;
+  const uint32_t chunk = p->sample_chunk ? p->sample_chunk : 64;
   for (uint32_t y = y0; y < y1; ++y) {
     const float f_y = (float)y;
     for (uint32_t x = 0; x < p->height; ++x) {  /* raytrace.zig:168 bound */
       const uint64_t offset = (uint64_t)y * p->width + x;
       V3 acc = v3(0.0f, 0.0f, 0.0f);
+      V3 chunk_acc = v3(0.0f, 0.0f, 0.0f);
       for (uint32_t s = 0; s < p->samples_per_pixel; ++s) {
         zs_rng local;
         if (p->rng_mode == ZRT_RNG_COUNTER) {
@@ -637,7 +639,17 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
         const float v = (f_y + zs_random_float(c.rng) - 0.5f) / f_height;
         const Ray ray = camera_get_ray(camera, u, v);
         const V3 col = ray_color(&c, &ray, p->max_depth);
-        acc.x += col.x; acc.y += col.y; acc.z += col.z;
+        if (p->rng_mode == ZRT_RNG_COUNTER) {
+          /* zrt.h sample_chunk: chunk sums, added in chunk order */
+          chunk_acc.x += col.x; chunk_acc.y += col.y; chunk_acc.z += col.z;
+          if ((s + 1) % chunk == 0 || s + 1 == p->samples_per_pixel) {
+            acc.x += chunk_acc.x; acc.y += chunk_acc.y; acc.z += chunk_acc.z;
+            chunk_acc = v3(0.0f, 0.0f, 0.0f);
+          }
+        } else {
+          /* raytrace.zig:177 color_acc.addMutate: one sequential sum */
+          acc.x += col.x; acc.y += col.y; acc.z += col.z;
+        }
         c.p.samples++;
       }
       c.p.pixels++;

@@ -25,7 +25,9 @@
  *     every scatter draw) — the reference algorithm as written.
  *   ZRT_RNG_COUNTER: the same arithmetic, but every (pixel, sample) starts its
  *     own stream, DefaultPrng.init(((y*width+x) << 16 | sample) + seed*0x9E3779B97F4A7C15).
- *     This is the bit-for-bit partner of the GPU kernel.
+ *     The per-pixel sum is taken in chunks of params->sample_chunk samples
+ *     (zrt.h), the kernel's unit of work.  This is the bit-for-bit partner of
+ *     the GPU kernel.
  */
 #ifndef ZRT_ORACLE_H
 #define ZRT_ORACLE_H

@@ -195,3 +195,15 @@ def test_bench_config_properties(scenes):
     for y in (0, 1024, 2047):  # one full row each, 2048 x 16 samples
         ref, _ = O.render(s.view, s.camera, p, rows=(y, y + 1))
         assert_bit_exact(img[y:y + 1], ref[y:y + 1])
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64, 100])
+def test_sample_chunks(scenes, chunk):
+    """zrt.h sample_chunk: chunk sums in chunk order; chunk >= spp is the
+    reference's single sequential sum (raytrace.zig:177)."""
+    s = scenes(1)
+    p = z.RenderParams(16, 16, 100, 30, sample_chunk=chunk)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    assert gs["samples_processed"] == rs["samples_processed"] == 16 * 16 * 100

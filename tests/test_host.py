@@ -41,7 +41,7 @@ def test_abi_version_and_struct_sizes():
     assert lib.zrt_abi_version() == 1
     assert b"gfx950" in lib.zrt_build_info()
     assert C.sizeof(_ffi.Prim) == 60 and C.sizeof(_ffi.Camera) == 48
-    assert C.sizeof(_ffi.Params) == 56 and C.sizeof(_ffi.BvhNode) == 32
+    assert C.sizeof(_ffi.Params) == 64 and C.sizeof(_ffi.BvhNode) == 32
 
 
 @pytest.mark.parametrize("index,n_prims", [(0, 1 + 3933), (1, 7), (2, 1 + 4968), (3, 1 + 6320), (4, 3 + 6320)])

@@ -47,6 +47,7 @@ class RenderParams:
     rank: int = 0
     world_size: int = 1
     device: int = 0
+    sample_chunk: int = 0
 
     def abi(self) -> _ffi.Params:
         p = _ffi.Params()
@@ -56,6 +57,7 @@ class RenderParams:
         p.rng_mode, p.prng, p.traversal = self.rng_mode, self.prng, self.traversal
         p.seed = self.seed
         p.rank, p.world_size, p.device = self.rank, self.world_size, self.device
+        p.sample_chunk = self.sample_chunk
         p.flags = 0
         return p
 

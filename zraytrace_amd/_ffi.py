@@ -72,7 +72,8 @@ class Params(C.Structure):
                 ("bounded_volume_hierarchy", C.c_uint32), ("rng_mode", C.c_uint32),
                 ("prng", C.c_uint32), ("traversal", C.c_uint32), ("seed", C.c_uint64),
                 ("rank", C.c_uint32), ("world_size", C.c_uint32),
-                ("device", C.c_uint32), ("flags", C.c_uint32)]
+                ("device", C.c_uint32), ("sample_chunk", C.c_uint32),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -80,6 +81,8 @@ class Stats(C.Structure):
                 ("background_hits", C.c_uint64), ("pixels_processed", C.c_uint64),
                 ("samples_processed", C.c_uint64), ("rays_processed", C.c_uint64),
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("sphere_tests", C.c_uint64), ("shade_fetches", C.c_uint64),
+                ("texel_fetches", C.c_uint64),
                 ("preprocess_ms", C.c_double), ("upload_ms", C.c_double),
                 ("render_ms", C.c_double), ("gather_ms", C.c_double),
                 ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),

@@ -62,17 +62,23 @@ struct KArgs {
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;
   float4* __restrict__ att;            // [max_depth][n_lanes]
-  float* __restrict__ out;             // this rank's tiles, tile-major, 64 px x RGB
+  float4* __restrict__ partial;        // [tile slot][chunk] chunk sums
   uint32_t* __restrict__ work_counter;
-  unsigned long long* __restrict__ counters;  // 6 x u64
+  unsigned long long* __restrict__ counters;  // kNumCounters x u64
   uint32_t* __restrict__ error_flag;
   float org[3], llc[3], hor[3], ver[3];
   float f_width, f_height, color_scale, pad0;
   uint32_t width, height, xbound, spp, max_depth;
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
+  uint32_t chunk, n_chunks;
   unsigned long long seed_mix;
 };
+
+// counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
+enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
+       kNumCounters };
+constexpr int kWorkSlot = 14, kErrorSlot = 15, kScratchSlots = 16;
 
 constexpr int kBlock = 256;
 
@@ -256,12 +262,16 @@ __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT
 
 template <bool TIE>
 __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int ref, const RayT& r,
-                                          float& best_t, int& best, uint32_t& c_prims) {
+                                          float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph) {
   const int code = -ref - 1;
   const int slot = code >> 1;
-  ++c_prims;
-  if (code & 1) tri_test<TIE>(prims, slot, r, best_t, best);
-  else sphere_test<TIE>(prims[3 * slot], slot, r, best_t, best);
+  if (code & 1) {
+    ++c_tri;
+    tri_test<TIE>(prims, slot, r, best_t, best);
+  } else {
+    ++c_sph;
+    sphere_test<TIE>(prims[3 * slot], slot, r, best_t, best);
+  }
 }
 
 __device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
@@ -271,7 +281,7 @@ __device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
 template <bool FAST>
 __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int* __restrict__ stk,
                                              float& best_t, int& best, uint32_t& c_nodes,
-                                             uint32_t& c_prims) {
+                                             uint32_t& c_tri, uint32_t& c_sph) {
   const int stride = kBlock;
   uint32_t sp = 0;
   const uint32_t cap = a.stack_depth;
@@ -283,8 +293,8 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
-        prim_test<true>(a.prims, left, r, best_t, best, c_prims);
-        if (right != left) prim_test<true>(a.prims, right, r, best_t, best, c_prims);
+        prim_test<true>(a.prims, left, r, best_t, best, c_tri, c_sph);
+        if (right != left) prim_test<true>(a.prims, right, r, best_t, best, c_tri, c_sph);
       } else {
         const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
         const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
@@ -334,8 +344,8 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
       if (!box_test<false>(lo, hi, r, best_t, &e)) continue;
       const int left = as_int(lo.w), right = as_int(hi.w);
       if (left < 0) {
-        prim_test<false>(a.prims, left, r, best_t, best, c_prims);
-        if (right != left) prim_test<false>(a.prims, right, r, best_t, best, c_prims);
+        prim_test<false>(a.prims, left, r, best_t, best, c_tri, c_sph);
+        if (right != left) prim_test<false>(a.prims, right, r, best_t, best, c_tri, c_sph);
       } else {
         if (sp + 2 <= cap) {
           stk[sp * stride] = right;
@@ -418,14 +428,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
   const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
 
   bool need = true, done = false, in_sample = false;
-  uint32_t work = 0, px = 0, py = 0, sample = 0;
+  uint32_t work = 0, px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
   uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
   uint32_t depth_left = 0, nb = 0;
   Rng<PRNG> rng;
   rng.init(0);
-  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_prims = 0;
+  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
+  uint32_t c_shade = 0, c_tex = 0;
+  const uint32_t per_tile = 64u * a.n_chunks;
 
   for (;;) {
     // ---- refill lanes whose pixel is finished: one atomic per wave
@@ -441,22 +453,22 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
         if (work >= a.total_work) {
           done = true;
         } else {
-          // tile-major work: local tile lt of this rank = global tile lt*world + rank
-          const uint32_t lt = work >> 6, p = work & 63u;
+          // work = (local tile lt, chunk j, pixel p); local tile lt of this
+          // rank is global tile lt*world + rank; the 64 pixels of one tile
+          // and chunk are consecutive, so a wave starts on one 8x8 tile.
+          const uint32_t lt = work / per_tile, rem = work - lt * per_tile;
+          const uint32_t j = rem >> 6, p = rem & 63u;
           const uint32_t t = lt * a.world + a.rank;
           px = (t % a.tiles_x) * 8u + (p & 7u);
           py = (t / a.tiles_x) * 8u + (p >> 3);
-          if (px < a.xbound && py < a.height) {
+          if (px < a.xbound && py < a.height) {  // else: finalize writes black
             need = false;
-            sample = 0;
+            slot = (lt * 64u + p) * a.n_chunks + j;
+            sample = j * a.chunk;
+            sample_end = min(sample + a.chunk, a.spp);
             acc_r = acc_g = acc_b = 0.0f;
             in_sample = false;
             offset = (uint64_t)py * a.width + px;
-          } else {
-            float* o3 = a.out + 3ull * work;  // outside the rendered area: black
-            o3[0] = 0.0f;
-            o3[1] = 0.0f;
-            o3[2] = 0.0f;
           }
         }
       }
@@ -496,12 +508,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
       if (MODE == 0) {
         for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order, t_max shrinking
           const uint32_t tag = __float_as_uint(a.shade[i].w);
-          if (tag >> 31) tri_test<false>(a.prims, (int)i, r, best_t, best);
-          else sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
-          ++c_prims;
+          if (tag >> 31) {
+            ++c_tri;
+            tri_test<false>(a.prims, (int)i, r, best_t, best);
+          } else {
+            ++c_sph;
+            sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
+          }
         }
       } else {
-        traverse_bvh<MODE == 1>(a, r, stk, best_t, best, c_nodes, c_prims);
+        traverse_bvh<MODE == 1>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
       if (best < 0) {
         ++c_bg;
@@ -514,6 +530,8 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
         const uint32_t tag = __float_as_uint(sh.w);
         const DevMaterial mat = a.mats[tag & 0x7fffffffu];
         const bool need_uv = mat.kind != ZRT_MAT_DIELECTRIC && mat.tex_kind == ZRT_TEX_IMAGE;
+        ++c_shade;
+        c_tex += need_uv ? 1u : 0u;
         const V3 loc = add(o, scale(d, best_t));
         V3 outward;
         float tu = 0.0f, tv = 0.0f;
@@ -605,22 +623,51 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
       acc_g += col.y;
       acc_b += col.z;
       in_sample = false;
-      if (++sample == a.spp) {
-        float* o3 = a.out + 3ull * work;
-        o3[0] = acc_r * a.color_scale;
-        o3[1] = acc_g * a.color_scale;
-        o3[2] = acc_b * a.color_scale;
+      if (++sample == sample_end) {  // chunk done: its sequential sum
+        a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
         need = true;
       }
     }
   }
 
-  wave_add_u64(&a.counters[0], c_depth);
-  wave_add_u64(&a.counters[1], c_refl);
-  wave_add_u64(&a.counters[2], c_bg);
-  wave_add_u64(&a.counters[3], c_rays);
-  wave_add_u64(&a.counters[4], c_nodes);
-  wave_add_u64(&a.counters[5], c_prims);
+  wave_add_u64(&a.counters[kDepthHits], c_depth);
+  wave_add_u64(&a.counters[kReflections], c_refl);
+  wave_add_u64(&a.counters[kBackground], c_bg);
+  wave_add_u64(&a.counters[kRays], c_rays);
+  wave_add_u64(&a.counters[kNodes], c_nodes);
+  wave_add_u64(&a.counters[kTriTests], c_tri);
+  wave_add_u64(&a.counters[kSphereTests], c_sph);
+  wave_add_u64(&a.counters[kShades], c_shade);
+  wave_add_u64(&a.counters[kTexels], c_tex);
+}
+
+// Per-pixel sum of the chunk sums in chunk order, times 1/spp
+// (raytrace.zig:182), into the rank's tile-major output.
+__global__ void finalize_kernel(const float4* __restrict__ partial, float* __restrict__ out,
+                                uint32_t n_slots, uint32_t n_chunks, uint32_t world, uint32_t rank,
+                                uint32_t tiles_x, uint32_t xbound, uint32_t height, float color_scale) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_slots) return;
+  const uint32_t lt = i >> 6, p = i & 63u;
+  const uint32_t t = lt * world + rank;
+  const uint32_t px = (t % tiles_x) * 8u + (p & 7u);
+  const uint32_t py = (t / tiles_x) * 8u + (p >> 3);
+  float r = 0.0f, g = 0.0f, b = 0.0f;
+  if (px < xbound && py < height) {
+    const float4* q = partial + (size_t)i * n_chunks;
+    for (uint32_t j = 0; j < n_chunks; ++j) {
+      const float4 v = q[j];
+      r += v.x;
+      g += v.y;
+      b += v.z;
+    }
+    r *= color_scale;
+    g *= color_scale;
+    b *= color_scale;
+  }
+  out[3ull * i + 0] = r;
+  out[3ull * i + 1] = g;
+  out[3ull * i + 2] = b;
 }
 
 // Scatter gathered rank tiles into the framebuffer (raytrace.zig:182 layout).
@@ -771,6 +818,7 @@ int validate_params(const zrt_params* p) {
   if (p->prng > ZRT_PRNG_XOSHIRO256) return fail(ZRT_E_INVALID, "unknown prng");
   if (p->traversal > ZRT_TRAVERSAL_REFERENCE) return fail(ZRT_E_INVALID, "unknown traversal");
   if (p->world_size == 0 || p->rank >= p->world_size) return fail(ZRT_E_INVALID, "rank must be < world_size");
+  if (p->sample_chunk > 65535) return fail(ZRT_E_INVALID, "sample_chunk must be <= 65535");
   return ZRT_OK;
 }
 
@@ -801,7 +849,8 @@ struct zrt_ctx {
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
   zrt::DevBuf<float4> att;
-  zrt::DevBuf<unsigned long long> scratch;  // [0..5] counters, [6] work counter, [7] error
+  zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
+  zrt::DevBuf<float4> partial;
   zrt::DevBuf<uint32_t> rank_base;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double preprocess_ms = 0, upload_ms = 0;
@@ -987,7 +1036,7 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
     // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
     zrt::build_device_scene(c.get(), scene, use_bvh);
-    c->scratch.alloc(8);
+    c->scratch.alloc(zrt::kScratchSlots);
     *out = c.release();
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
@@ -1008,7 +1057,8 @@ int zrt_ctx_destroy(zrt_ctx* ctx) {
 }
 
 int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n_tiles) {
-  if (!ctx || !n_tiles) return fail(ZRT_E_INVALID, "null argument");
+  (void)ctx;  // the partition depends on the params only; ctx may be NULL
+  if (!n_tiles) return fail(ZRT_E_INVALID, "null argument");
   const int rc = zrt::validate_params(params);
   if (rc) return rc;
   *n_tiles = zrt::rank_tiles(zrt::geometry(params), params->rank, params->world_size);
@@ -1032,14 +1082,20 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
     uint32_t grid = uint32_t(c->cu_count) * uint32_t(per_cu);
-    const uint32_t work = my_tiles * 64u;
+    const uint32_t chunk = p->sample_chunk ? p->sample_chunk : 64u;
+    const uint32_t n_chunks = (p->samples_per_pixel + chunk - 1) / chunk;
+    const uint64_t work64 = uint64_t(my_tiles) * 64u * n_chunks;
+    if (work64 >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "more than 2^32 (pixel, chunk) work units");
+    const uint32_t work = uint32_t(work64);
     grid = std::max(1u, std::min(grid, (work + zrt::kBlock - 1) / zrt::kBlock));
+    const uint64_t n_partial = uint64_t(my_tiles) * 64u * n_chunks;
+    if (c->partial.n < n_partial) c->partial.alloc(n_partial);
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
     const uint64_t att_need = std::max<uint64_t>(1, p->max_depth) * n_lanes;
     if (att_need * sizeof(float4) > (16ull << 30))
       return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
     if (c->att.n < att_need) c->att.alloc(att_need);
-    HIPCHK(hipMemsetAsync(c->scratch.p, 0, 8 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(c->scratch.p, 0, zrt::kScratchSlots * sizeof(unsigned long long), st));
 
     zrt::KArgs a{};
     a.nodes = c->nodes.p;
@@ -1048,10 +1104,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.mats = c->mats.p;
     a.texels = c->texels.p;
     a.att = c->att.p;
-    a.out = dev_tiles;
+    a.partial = c->partial.p;
     a.counters = c->scratch.p;
-    a.work_counter = reinterpret_cast<uint32_t*>(c->scratch.p + 6);
-    a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + 7);
+    a.work_counter = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kWorkSlot);
+    a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
     const zrt_vec3* v[4] = {&cam->origin, &cam->lower_left_corner, &cam->horizontal, &cam->vertical};
     float* dst[4] = {a.org, a.llc, a.hor, a.ver};
     for (int k = 0; k < 4; ++k) {
@@ -1075,6 +1131,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.stack_depth = c->stack_depth;
     a.n_lanes = uint32_t(n_lanes);
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
+    a.chunk = chunk;
+    a.n_chunks = n_chunks;
 
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
@@ -1082,6 +1140,13 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       HIPCHK(hipLaunchKernel(kfn, dim3(grid), dim3(zrt::kBlock), args, lds, st));
     }
     HIPCHK(hipEventRecord(c->ev1, st));
+    if (my_tiles > 0) {
+      const uint32_t n_slots = my_tiles * 64u;
+      hipLaunchKernelGGL(zrt::finalize_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st, c->partial.p,
+                         dev_tiles, n_slots, n_chunks, p->world_size, p->rank, g.tiles_x, g.xbound, p->height,
+                         a.color_scale);
+      HIPCHK(hipGetLastError());
+    }
     // count the pixels this rank renders (for samples/pixels counters)
     uint64_t pixels = 0;
     for (uint32_t lt = 0; lt < my_tiles; ++lt) {
@@ -1101,18 +1166,23 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
 
 int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
   if (!c || !out) return fail(ZRT_E_INVALID, "null argument");
+  if (!c->launched) return fail(ZRT_E_INVALID, "zrt_ctx_stats before any zrt_ctx_render_tiles");
   try {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipEventSynchronize(c->ev1));
-    unsigned long long h[8] = {0};
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long h[zrt::kScratchSlots] = {0};
     HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof(*out));
-    out->recursion_depth_hits = h[0];
-    out->reflections = h[1];
-    out->background_hits = h[2];
-    out->rays_processed = h[3];
-    out->node_visits = h[4];
-    out->prim_tests = h[5];
+    out->recursion_depth_hits = h[zrt::kDepthHits];
+    out->reflections = h[zrt::kReflections];
+    out->background_hits = h[zrt::kBackground];
+    out->rays_processed = h[zrt::kRays];
+    out->node_visits = h[zrt::kNodes];
+    out->prim_tests = h[zrt::kTriTests] + h[zrt::kSphereTests];
+    out->sphere_tests = h[zrt::kSphereTests];
+    out->shade_fetches = h[zrt::kShades];
+    out->texel_fetches = h[zrt::kTexels];
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
     out->preprocess_ms = c->preprocess_ms;
@@ -1124,7 +1194,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->bvh_nodes = c->n_nodes;
     out->bvh_max_depth = c->bvh_depth;
     out->n_gpus = 1;
-    if (h[7] != 0) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
+    if (h[zrt::kErrorSlot] != 0) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
@@ -1133,6 +1203,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
 
 int zrt_ctx_last_kernel_ms(zrt_ctx* c, double* ms) {
   if (!c || !ms) return fail(ZRT_E_INVALID, "null argument");
+  if (!c->launched) return fail(ZRT_E_INVALID, "no kernel launched on this context yet");
   try {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipEventSynchronize(c->ev1));
