@@ -143,7 +143,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    st = ctx.stats()  # counters of the last launch (identical every step: deterministic)
+    st = ctx.stats()  # Progress counters of the last timed launch (identical every step)
+    # Traffic diagnostics (node visits, primitive tests, ...) come from one extra,
+    # untimed launch of the diagnostic kernel flavour: same traversal, same image.
+    pdiag = z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS})
+    ctx.render_tiles(scene.camera, pdiag, tiles.data_ptr(), stream)
+    diag = ctx.stats()
+    diag_kernel_ms = ctx.kernel_ms()
+    assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
     rays = torch.tensor([float(st["rays_processed"]), float(st["samples_processed"])], dtype=torch.float64,
                         device="cuda")
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -158,7 +165,7 @@ def main():
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
         chunk = args.chunk or 64
         n_units = my_tiles * 64 * ((args.spp + chunk - 1) // chunk)
-        algo = algorithmic_bytes(st, n_units, st["pixels_processed"])
+        algo = algorithmic_bytes(diag, n_units, diag["pixels_processed"])
         achieved = algo / avg_kernel_s / 1e9
         pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
@@ -192,9 +199,11 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": "render_kernel<1,0> (BVH fast traversal)",
                          "algorithmic_bytes_per_launch": int(algo),
-                         "per_ray": {"node_visits": round(st["node_visits"] / max(1, st["rays_processed"]), 2),
-                                     "prim_tests": round(st["prim_tests"] / max(1, st["rays_processed"]), 2),
-                                     "bytes": round(algo / max(1, st["rays_processed"]), 1)}},
+                         "per_ray": {"node_visits": round(diag["node_visits"] / max(1, diag["rays_processed"]), 2),
+                                     "prim_tests": round(diag["prim_tests"] / max(1, diag["rays_processed"]), 2),
+                                     "bytes": round(algo / max(1, diag["rays_processed"]), 1)},
+                         "counters_from": "one untimed ZRT_FLAG_STATS launch (kernel "
+                                          f"{diag_kernel_ms:.1f} ms)"},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -152,9 +152,15 @@ typedef struct zrt_params {
    * sample_chunk >= samples_per_pixel this is the reference's single
    * sequential sum.  A chunk is the kernel's unit of work. */
   uint32_t sample_chunk;
-  uint32_t flags;                    /* reserved, 0 */
+  uint32_t flags;                    /* ZRT_FLAG_* */
   uint32_t reserved;
 } zrt_params;
+
+/* flags: ZRT_FLAG_STATS launches the diagnostic flavour of the kernel that also
+ * counts BVH node visits, primitive tests, shaded hits and texel fetches
+ * (zrt_stats).  Images are identical; the default flavour counts only the
+ * Progress counters (raytrace.zig:20-34). */
+enum { ZRT_FLAG_STATS = 1u };
 
 /* Progress counters (raytrace.zig:20-34) + timings. */
 typedef struct zrt_stats {

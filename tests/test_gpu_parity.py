@@ -92,6 +92,12 @@ def test_render_bit_exact_vs_oracle(scenes, case, traversal):
     assert_bit_exact(gpu, ref)
     for k in COUNTERS:
         assert gs[k] == rs[k], k
+    # the diagnostic flavour renders the same image and counts rays directly
+    p.flags = z.ZRT_FLAG_STATS
+    gpu2, gs = z.render(s, s.camera, p)
+    assert same_bits(gpu, gpu2).all()
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
     if traversal == z.ZRT_TRAVERSAL_REFERENCE and rs["used_bvh"]:
         # the same DFS with the same slab tests visits the same nodes
         assert gs["node_visits"] == rs["node_visits"]

@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _ffi
 from ._ffi import (ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256, ZRT_RNG_COUNTER,  # noqa: F401
-                   ZRT_RNG_REFERENCE_STREAM, ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE,
+                   ZRT_RNG_REFERENCE_STREAM, ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE, ZRT_FLAG_STATS,
                    ZrtError, check)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -48,6 +48,7 @@ class RenderParams:
     world_size: int = 1
     device: int = 0
     sample_chunk: int = 0
+    flags: int = 0
 
     def abi(self) -> _ffi.Params:
         p = _ffi.Params()
@@ -58,7 +59,7 @@ class RenderParams:
         p.seed = self.seed
         p.rank, p.world_size, p.device = self.rank, self.world_size, self.device
         p.sample_chunk = self.sample_chunk
-        p.flags = 0
+        p.flags = self.flags
         return p
 
 

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzrt.so")
+# ZRT_LIB overrides the library path (A/B of build variants, tools/variants.sh)
+LIB_PATH = os.environ.get("ZRT_LIB") or os.path.join(HERE, "libzrt.so")
 
 # ---- status / enums (zrt.h) --------------------------------------------------
 ZRT_OK = 0
@@ -28,6 +29,7 @@ ZRT_TEX_COLOR, ZRT_TEX_IMAGE = 0, 1
 ZRT_RNG_COUNTER, ZRT_RNG_REFERENCE_STREAM = 0, 1
 ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256 = 0, 1
 ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE = 0, 1
+ZRT_FLAG_STATS = 1
 
 
 class Vec3(C.Structure):

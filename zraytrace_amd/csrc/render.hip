@@ -260,16 +260,16 @@ __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT
   }
 }
 
-template <bool TIE>
+template <bool TIE, bool STATS>
 __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int ref, const RayT& r,
                                           float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph) {
   const int code = -ref - 1;
   const int slot = code >> 1;
   if (code & 1) {
-    ++c_tri;
+    if (STATS) ++c_tri;
     tri_test<TIE>(prims, slot, r, best_t, best);
   } else {
-    ++c_sph;
+    if (STATS) ++c_sph;
     sphere_test<TIE>(prims[3 * slot], slot, r, best_t, best);
   }
 }
@@ -278,8 +278,8 @@ __device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
 
 // Closest hit over the BVH.  FAST: near-first order with the narrowed slab
 // test; REFERENCE: left-first DFS with exactly bvh.zig:187-205's tests.
-template <bool FAST>
-__device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int* __restrict__ stk,
+template <bool FAST, bool STATS, class StackT>
+__device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                              float& best_t, int& best, uint32_t& c_nodes,
                                              uint32_t& c_tri, uint32_t& c_sph) {
   const int stride = kBlock;
@@ -288,17 +288,17 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
   if (FAST) {
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
-    ++c_nodes;
+    if (STATS) ++c_nodes;
     if (!box_test<true>(lo, hi, r, best_t * 1.0000153f, &e)) return;
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
-        prim_test<true>(a.prims, left, r, best_t, best, c_tri, c_sph);
-        if (right != left) prim_test<true>(a.prims, right, r, best_t, best, c_tri, c_sph);
+        prim_test<true, STATS>(a.prims, left, r, best_t, best, c_tri, c_sph);
+        if (right != left) prim_test<true, STATS>(a.prims, right, r, best_t, best, c_tri, c_sph);
       } else {
         const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
         const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
-        c_nodes += 2;
+        if (STATS) c_nodes += 2;
         const float tb = best_t * 1.0000153f;
         float el, er;
         const bool hl = box_test<true>(l0, l1, r, tb, &el);
@@ -306,7 +306,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
         if (hl && hr) {
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
-          if (sp < cap) stk[sp * stride] = far_idx;
+          if (sp < cap) stk[sp * stride] = (StackT)far_idx;
           else atomicOr(a.error_flag, 1u);
           ++sp;
           left = rfirst ? as_int(r0.w) : as_int(l0.w);
@@ -322,7 +322,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
         --sp;
         const int idx = sp < cap ? stk[sp * stride] : 0;
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
-        ++c_nodes;
+        if (STATS) ++c_nodes;
         if (box_test<true>(p0, p1, r, best_t * 1.0000153f, &e)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
@@ -339,17 +339,17 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, int*
       --sp;
       const int idx = stk[sp * stride];
       const float4 lo = a.nodes[2 * idx], hi = a.nodes[2 * idx + 1];
-      ++c_nodes;
+      if (STATS) ++c_nodes;
       float e;
       if (!box_test<false>(lo, hi, r, best_t, &e)) continue;
       const int left = as_int(lo.w), right = as_int(hi.w);
       if (left < 0) {
-        prim_test<false>(a.prims, left, r, best_t, best, c_tri, c_sph);
-        if (right != left) prim_test<false>(a.prims, right, r, best_t, best, c_tri, c_sph);
+        prim_test<false, STATS>(a.prims, left, r, best_t, best, c_tri, c_sph);
+        if (right != left) prim_test<false, STATS>(a.prims, right, r, best_t, best, c_tri, c_sph);
       } else {
         if (sp + 2 <= cap) {
-          stk[sp * stride] = right;
-          stk[(sp + 1) * stride] = left;
+          stk[sp * stride] = (StackT)right;
+          stk[(sp + 1) * stride] = (StackT)left;
           sp += 2;
         } else {
           atomicOr(a.error_flag, 1u);
@@ -372,9 +372,30 @@ __device__ __forceinline__ uint32_t texel_index(float f, uint32_t n) {
   return n - 1;
 }
 
+// A material: the {u_off, v_off, kind, tex_kind} quad is read at the hit;
+// color / image descriptor are read where the albedo is needed (keeping the
+// whole 48-B record live across scatter spilled it to scratch).
+struct MatReg {
+  const float4* q;
+  float4 m1;  // {u_off, v_off, kind, tex_kind}
+  __device__ __forceinline__ uint32_t kind() const { return __float_as_uint(m1.z); }
+  __device__ __forceinline__ uint32_t tex_kind() const { return __float_as_uint(m1.w); }
+  __device__ __forceinline__ float ior() const { return q[0].w; }
+};
+__device__ __forceinline__ MatReg load_material(const DevMaterial* __restrict__ mats, uint32_t i) {
+  const float4* q = reinterpret_cast<const float4*>(mats + i);
+  return MatReg{q, q[1]};
+}
+
 // texture.zig:20-74
-__device__ __forceinline__ V3 albedo(const DevMaterial& m, const float* __restrict__ texels, float u, float v) {
-  if (m.tex_kind == ZRT_TEX_COLOR) return mk(m.r, m.g, m.b);
+__device__ __forceinline__ V3 albedo(const MatReg& mr, const float* __restrict__ texels, float u, float v) {
+  if (mr.tex_kind() == ZRT_TEX_COLOR) {
+    const float4 c = mr.q[0];
+    return mk(c.x, c.y, c.z);
+  }
+  const float4 m2 = mr.q[2];
+  struct { float u_off, v_off; uint32_t img_w, img_h, img_off; } m = {
+      mr.m1.x, mr.m1.y, __float_as_uint(m2.x), __float_as_uint(m2.y), __float_as_uint(m2.z)};
   const float uu_first = 1.0f - u + m.u_off;
   float uu = uu_first;
   if (uu_first > 1.0f) uu = uu_first - 1.0f;
@@ -420,10 +441,15 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
 constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 
-template <int MODE /*0 list, 1 BVH fast, 2 BVH reference*/, int PRNG>
-__global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
-  extern __shared__ int lds_stack[];
-  int* stk = lds_stack + threadIdx.x;
+// StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
+// more blocks fit per CU), uint32_t otherwise.
+template <int MODE /*0 list, 1 BVH fast, 2 BVH reference*/, int PRNG, bool STATS, class StackT>
+#ifndef ZRT_WAVES_PER_SIMD
+#define ZRT_WAVES_PER_SIMD 8  // A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
+#endif
+__global__ void __launch_bounds__(kBlock, ZRT_WAVES_PER_SIMD) render_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
   const int lane = (int)__lane_id();
   const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
 
@@ -498,7 +524,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
       ++c_depth;
       path_end = true;
     } else {
-      ++c_rays;
+      if (STATS) ++c_rays;
       RayT r;
       r.ox = o.x; r.oy = o.y; r.oz = o.z;
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
@@ -509,15 +535,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
         for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order, t_max shrinking
           const uint32_t tag = __float_as_uint(a.shade[i].w);
           if (tag >> 31) {
-            ++c_tri;
+            if (STATS) ++c_tri;
             tri_test<false>(a.prims, (int)i, r, best_t, best);
           } else {
-            ++c_sph;
+            if (STATS) ++c_sph;
             sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
           }
         }
       } else {
-        traverse_bvh<MODE == 1>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
+        traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
       if (best < 0) {
         ++c_bg;
@@ -528,10 +554,13 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
         // ---- HitRecord.init (hit_record.zig:28-41)
         const float4 sh = a.shade[best];
         const uint32_t tag = __float_as_uint(sh.w);
-        const DevMaterial mat = a.mats[tag & 0x7fffffffu];
-        const bool need_uv = mat.kind != ZRT_MAT_DIELECTRIC && mat.tex_kind == ZRT_TEX_IMAGE;
-        ++c_shade;
-        c_tex += need_uv ? 1u : 0u;
+        const MatReg mat = load_material(a.mats, tag & 0x7fffffffu);
+        const uint32_t mkind = mat.kind();
+        const bool need_uv = mkind != ZRT_MAT_DIELECTRIC && mat.tex_kind() == ZRT_TEX_IMAGE;
+        if (STATS) {
+          ++c_shade;
+          c_tex += need_uv ? 1u : 0u;
+        }
         const V3 loc = add(o, scale(d, best_t));
         V3 outward;
         float tu = 0.0f, tv = 0.0f;
@@ -568,7 +597,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
         // ---- Material.scatter (material.zig:43-129)
         bool absorbed = false;
         V3 att = mk(1.0f, 1.0f, 1.0f), nd;
-        if (mat.kind == ZRT_MAT_LAMBERTIAN) {
+        if (mkind == ZRT_MAT_LAMBERTIAN) {
           const float r1 = rand_float(rng);
           const float r2 = rand_float(rng);
           const float rr = dev::sqrt_rn(1.0f - r1 * r1);
@@ -578,12 +607,12 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
           if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
           nd = unit(add(normal, hv));
           att = albedo(mat, a.texels, tu, tv);
-        } else if (mat.kind == ZRT_MAT_METAL) {
+        } else if (mkind == ZRT_MAT_METAL) {
           nd = unit(reflect(unit(d), normal));
           if (dot(nd, normal) > 0.0f) att = albedo(mat, a.texels, tu, tv);
           else absorbed = true;
         } else {
-          const float ratio = front ? (1.0f / mat.ior) : mat.ior;
+          const float ratio = front ? (1.0f / mat.ior()) : mat.ior();
           const V3 ud = unit(d);
           const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
           const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
@@ -633,12 +662,14 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KArgs a) {
   wave_add_u64(&a.counters[kDepthHits], c_depth);
   wave_add_u64(&a.counters[kReflections], c_refl);
   wave_add_u64(&a.counters[kBackground], c_bg);
-  wave_add_u64(&a.counters[kRays], c_rays);
-  wave_add_u64(&a.counters[kNodes], c_nodes);
-  wave_add_u64(&a.counters[kTriTests], c_tri);
-  wave_add_u64(&a.counters[kSphereTests], c_sph);
-  wave_add_u64(&a.counters[kShades], c_shade);
-  wave_add_u64(&a.counters[kTexels], c_tex);
+  if (STATS) {
+    wave_add_u64(&a.counters[kRays], c_rays);
+    wave_add_u64(&a.counters[kNodes], c_nodes);
+    wave_add_u64(&a.counters[kTriTests], c_tri);
+    wave_add_u64(&a.counters[kSphereTests], c_sph);
+    wave_add_u64(&a.counters[kShades], c_shade);
+    wave_add_u64(&a.counters[kTexels], c_tex);
+  }
 }
 
 // Per-pixel sum of the chunk sums in chunk order, times 1/spp
@@ -856,6 +887,7 @@ struct zrt_ctx {
   double preprocess_ms = 0, upload_ms = 0;
   // last launch
   uint32_t last_pixels = 0, last_spp = 0, launched = 0;
+  bool last_stats = false;
   int cu_count = 0;
   ~zrt_ctx() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -982,20 +1014,23 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
   c->stack_depth = use_bvh ? depth + 2 : 0;
 }
 
-template <int MODE, int PRNG>
+template <int MODE, int PRNG, bool STATS, class StackT>
 void* kernel_ptr() {
-  return reinterpret_cast<void*>(&render_kernel<MODE, PRNG>);
+  return reinterpret_cast<void*>(&render_kernel<MODE, PRNG, STATS, StackT>);
 }
 
-void* select_kernel(int mode, uint32_t prng) {
-  if (prng == ZRT_PRNG_XOSHIRO256) {
-    if (mode == 0) return kernel_ptr<0, ZRT_PRNG_XOSHIRO256>();
-    if (mode == 1) return kernel_ptr<1, ZRT_PRNG_XOSHIRO256>();
-    return kernel_ptr<2, ZRT_PRNG_XOSHIRO256>();
-  }
-  if (mode == 0) return kernel_ptr<0, ZRT_PRNG_XOROSHIRO128>();
-  if (mode == 1) return kernel_ptr<1, ZRT_PRNG_XOROSHIRO128>();
-  return kernel_ptr<2, ZRT_PRNG_XOROSHIRO128>();
+template <int PRNG, bool STATS>
+void* select_kernel_ps(int mode, bool stk16) {
+  if (mode == 0) return kernel_ptr<0, PRNG, STATS, uint16_t>();  // list mode: no stack
+  if (mode == 1) return stk16 ? kernel_ptr<1, PRNG, STATS, uint16_t>() : kernel_ptr<1, PRNG, STATS, uint32_t>();
+  return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
+}
+void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
+  if (prng == ZRT_PRNG_XOSHIRO256)
+    return stats ? select_kernel_ps<ZRT_PRNG_XOSHIRO256, true>(mode, stk16)
+                 : select_kernel_ps<ZRT_PRNG_XOSHIRO256, false>(mode, stk16);
+  return stats ? select_kernel_ps<ZRT_PRNG_XOROSHIRO128, true>(mode, stk16)
+               : select_kernel_ps<ZRT_PRNG_XOROSHIRO128, false>(mode, stk16);
 }
 
 int hip_fail(const HipError& e) {
@@ -1076,8 +1111,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const zrt::Geometry g = zrt::geometry(p);
     const uint32_t my_tiles = zrt::rank_tiles(g, p->rank, p->world_size);
     const int mode = !c->use_bvh ? 0 : (p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2 : 1);
-    void* kfn = zrt::select_kernel(mode, p->prng);
-    const size_t lds = size_t(c->stack_depth) * zrt::kBlock * sizeof(int);
+    const bool diag = (p->flags & ZRT_FLAG_STATS) != 0;
+    const bool stk16 = c->n_nodes < 65536;
+    void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
+    const size_t lds = size_t(c->stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
@@ -1157,6 +1194,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     }
     c->last_pixels = uint32_t(pixels);
     c->last_spp = p->samples_per_pixel;
+    c->last_stats = diag;
     c->launched = 1;
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
@@ -1177,7 +1215,10 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->recursion_depth_hits = h[zrt::kDepthHits];
     out->reflections = h[zrt::kReflections];
     out->background_hits = h[zrt::kBackground];
-    out->rays_processed = h[zrt::kRays];
+    // rayColor calls = samples + reflections = rays + depth-limit hits
+    out->rays_processed = c->last_stats ? h[zrt::kRays]
+                                        : uint64_t(c->last_pixels) * c->last_spp + h[zrt::kReflections] -
+                                              h[zrt::kDepthHits];
     out->node_visits = h[zrt::kNodes];
     out->prim_tests = h[zrt::kTriTests] + h[zrt::kSphereTests];
     out->sphere_tests = h[zrt::kSphereTests];
