@@ -34,12 +34,13 @@ def log(*a):
 
 def algorithmic_bytes(st, n_work_units, n_pixels):
     """Bytes the sampling loop must touch per launch:
-    32 B per BVH node tested, 48 B per triangle test, 16 B per sphere test,
+    per node record read (32 B binary/reference node, 128 B wide node), 32 B
+    per reference leaf opened (wide traversal), 48 B per triangle test, 16 B per sphere test,
     64 B per shaded hit (16 B shade record + 48 B material), 12 B per texel,
     32 B per scatter (attenuation pushed + read back), 16 B per chunk sum
     written and read, 12 B per output pixel."""
     tri = st["prim_tests"] - st["sphere_tests"]
-    return (32 * st["node_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
+    return (st["node_bytes"] * st["node_visits"] + 32 * st["leaf_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
             + 12 * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 
@@ -86,7 +87,7 @@ def main():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--depth", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--traversal", choices=["fast", "reference"], default="fast")
+    ap.add_argument("--traversal", choices=["fast", "reference", "binary"], default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -104,7 +105,8 @@ def main():
 
     import zraytrace_amd as z
     scene = z.load_scene(args.scene)
-    trav = z.ZRT_TRAVERSAL_FAST if args.traversal == "fast" else z.ZRT_TRAVERSAL_REFERENCE
+    trav = {"fast": z.ZRT_TRAVERSAL_FAST, "reference": z.ZRT_TRAVERSAL_REFERENCE,
+            "binary": z.ZRT_TRAVERSAL_BINARY}[args.traversal]
     params = z.RenderParams(args.width, args.height, args.spp, args.depth, traversal=trav,
                             rank=rank, world_size=world, device=local, sample_chunk=args.chunk)
     ctx = z.RenderContext(scene, params)
@@ -197,9 +199,10 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_unit": "bytes per launch (rocprofv3 (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB)",
                          "traffic_source": traffic_src,
-                         "kernel": "render_kernel<1,0> (BVH fast traversal)",
+                         "kernel": f"render_kernel (BVH {args.traversal} traversal)",
                          "algorithmic_bytes_per_launch": int(algo),
                          "per_ray": {"node_visits": round(diag["node_visits"] / max(1, diag["rays_processed"]), 2),
+                                     "leaf_visits": round(diag["leaf_visits"] / max(1, diag["rays_processed"]), 2),
                                      "prim_tests": round(diag["prim_tests"] / max(1, diag["rays_processed"]), 2),
                                      "bytes": round(algo / max(1, diag["rays_processed"]), 1)},
                          "counters_from": "one untimed ZRT_FLAG_STATS launch (kernel "

@@ -129,8 +129,13 @@ enum {
 };
 enum { ZRT_PRNG_XOROSHIRO128 = 0, ZRT_PRNG_XOSHIRO256 = 1 };
 enum {
-  ZRT_TRAVERSAL_FAST = 0,       /* near-first, extra conservative slab prune, DFS tie-break */
-  ZRT_TRAVERSAL_REFERENCE = 1   /* left-first DFS with exactly bvh.zig:187-205's tests */
+  /* FAST: a 4-wide SAH tree built over the reference BVH's leaves culls with
+   * the narrowed slab test; every leaf reached is put through the reference's
+   * own slab test; equal-t ties go to the earlier leaf in the reference's DFS
+   * order.  Same answers as REFERENCE. */
+  ZRT_TRAVERSAL_FAST = 0,
+  ZRT_TRAVERSAL_REFERENCE = 1,  /* left-first DFS with exactly bvh.zig:187-205's tests */
+  ZRT_TRAVERSAL_BINARY = 2      /* near-first over the reference BVH itself, narrowed + loose tests */
 };
 
 typedef struct zrt_params {
@@ -175,6 +180,7 @@ typedef struct zrt_stats {
   uint64_t sphere_tests;  /* ... of which spheres */
   uint64_t shade_fetches; /* closest hits shaded (hit record + material reads) */
   uint64_t texel_fetches; /* image-texture lookups */
+  uint64_t leaf_visits;   /* FAST traversal: reference leaves opened (node_visits = wide nodes) */
   double preprocess_ms;   /* BVH build + flatten (raytrace.zig:150) */
   double upload_ms;
   double render_ms;       /* kernel time (HIP events) */
@@ -183,6 +189,8 @@ typedef struct zrt_stats {
   uint32_t bvh_nodes;
   uint32_t bvh_max_depth; /* Tracking.max_depth (bvh.zig:23-30) */
   uint32_t n_gpus;
+  uint32_t node_bytes;    /* bytes of one node record of the traversal used (32 or 128) */
+  uint32_t wide_nodes;    /* FAST traversal: 4-wide nodes over the reference leaves */
 } zrt_stats;
 
 /* ---- entry points -------------------------------------------------------- */

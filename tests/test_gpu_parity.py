@@ -81,7 +81,8 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("traversal", [z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE])
+@pytest.mark.parametrize("traversal", [z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE, z.ZRT_TRAVERSAL_BINARY],
+                         ids=["fast", "reference", "binary"])
 @pytest.mark.parametrize("case", CASES, ids=[f"scene{c[0]}" for c in CASES])
 def test_render_bit_exact_vs_oracle(scenes, case, traversal):
     idx, w, h, spp, depth = case

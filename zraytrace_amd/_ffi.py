@@ -28,7 +28,7 @@ ZRT_MAT_LAMBERTIAN, ZRT_MAT_METAL, ZRT_MAT_DIELECTRIC = 0, 1, 2
 ZRT_TEX_COLOR, ZRT_TEX_IMAGE = 0, 1
 ZRT_RNG_COUNTER, ZRT_RNG_REFERENCE_STREAM = 0, 1
 ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256 = 0, 1
-ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE = 0, 1
+ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE, ZRT_TRAVERSAL_BINARY = 0, 1, 2
 ZRT_FLAG_STATS = 1
 
 
@@ -84,11 +84,12 @@ class Stats(C.Structure):
                 ("samples_processed", C.c_uint64), ("rays_processed", C.c_uint64),
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("shade_fetches", C.c_uint64),
-                ("texel_fetches", C.c_uint64),
+                ("texel_fetches", C.c_uint64), ("leaf_visits", C.c_uint64),
                 ("preprocess_ms", C.c_double), ("upload_ms", C.c_double),
                 ("render_ms", C.c_double), ("gather_ms", C.c_double),
                 ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),
-                ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32)]
+                ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32),
+                ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -1,0 +1,271 @@
+// accel_build.cpp — a wide (4-ary) SAH tree over the reference's BVH leaves.
+//
+// Why this is exact.  The reference finds the closest hit by a left-first
+// recursion (bvh.zig:187-205) whose node test is aabb.zig:109-127: every axis
+// checked on its own against [t_min, t_max].  That test is monotone under box
+// containment: node boxes are exact min/max unions of their children
+// (bvh.zig:164), f32 rounding of (bound - origin) * (1/d) is monotone in the
+// bound, so if a leaf's box passes, every ancestor's box passes for the same
+// t_max (and the reference's t_max at an ancestor is never smaller than at the
+// leaf).  Hence the primitives the reference can return are exactly those in
+// leaves whose own box passes the loose test, and its answer is the minimum t
+// with ties to the earliest leaf in its DFS order.
+//
+// So the device may reach the reference's leaves through ANY tree of boxes that
+// contain them, culling with any test that never rejects a box containing a
+// hit closer than the current best (the narrowed slab test with a 2^-16
+// relative margin), as long as every leaf it opens is first put through the
+// reference's own loose test and ties go to the lower DFS slot.  This file
+// builds that tree: binned SAH (true surface area) over the reference leaves
+// as items, then collapsed to 4 children per node.
+//
+// Device layout (filled here, read by render.hip):
+//   wide node = 8 x float4 (128 B, one cache line):
+//     {min.x of children 0..3}, {min.y}, {min.z}, {max.x}, {max.y}, {max.z},
+//     {child refs (int bits)}, {unused}
+//     child ref >= 0: wide node index; ref < 0: reference leaf ~ref;
+//     an empty child slot has an empty box (min = +inf, max = -inf).
+//   reference leaf = 2 x float4 (32 B): {min.xyz, prim ref a}, {max.xyz, prim ref b}
+//     with the primitive-slot refs of render.hip (b == a for a one-primitive leaf).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "accel_build.hpp"
+
+namespace zrt {
+
+namespace {
+
+struct Aabb {
+  float mn[3] = {INFINITY, INFINITY, INFINITY};
+  float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Aabb& b) {
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = std::min(mn[k], b.mn[k]);
+      mx[k] = std::max(mx[k], b.mx[k]);
+    }
+  }
+  void grow(const float p[3]) {
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = std::min(mn[k], p[k]);
+      mx[k] = std::max(mx[k], p[k]);
+    }
+  }
+  double area() const {
+    if (mx[0] < mn[0]) return 0.0;
+    const double dx = double(mx[0]) - mn[0], dy = double(mx[1]) - mn[1], dz = double(mx[2]) - mn[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Item {
+  Aabb box;
+  float c[3];
+  int32_t leaf;
+};
+
+struct Node2 {
+  Aabb box;
+  int32_t left = -1, right = -1;  // children (Node2 indices); -1 for a leaf
+  int32_t leaf = -1;              // reference leaf index for a leaf
+};
+
+struct Builder2 {
+  std::vector<Item>& items;
+  std::vector<Node2> nodes;
+
+  int32_t build(size_t lo, size_t hi) {
+    const int32_t me = int32_t(nodes.size());
+    nodes.emplace_back();
+    Aabb box, cb;
+    for (size_t i = lo; i < hi; ++i) {
+      box.grow(items[i].box);
+      cb.grow(items[i].c);
+    }
+    nodes[me].box = box;
+    const size_t n = hi - lo;
+    if (n == 1) {
+      nodes[me].leaf = items[lo].leaf;
+      return me;
+    }
+    // binned SAH over centroids
+    constexpr int kBins = 32;
+    int best_axis = -1, best_bin = -1;
+    double best_cost = INFINITY;
+    for (int axis = 0; axis < 3; ++axis) {
+      const float ext = cb.mx[axis] - cb.mn[axis];
+      if (!(ext > 0.0f)) continue;
+      Aabb bb[kBins];
+      size_t cnt[kBins] = {0};
+      const float scale = kBins / ext;
+      for (size_t i = lo; i < hi; ++i) {
+        int b = int((items[i].c[axis] - cb.mn[axis]) * scale);
+        b = std::min(std::max(b, 0), kBins - 1);
+        bb[b].grow(items[i].box);
+        ++cnt[b];
+      }
+      double right_area[kBins];
+      size_t right_cnt[kBins];
+      Aabb acc;
+      size_t c = 0;
+      for (int b = kBins - 1; b > 0; --b) {
+        acc.grow(bb[b]);
+        c += cnt[b];
+        right_area[b] = acc.area();
+        right_cnt[b] = c;
+      }
+      Aabb lacc;
+      size_t lc = 0;
+      for (int b = 0; b < kBins - 1; ++b) {
+        lacc.grow(bb[b]);
+        lc += cnt[b];
+        if (lc == 0 || right_cnt[b + 1] == 0) continue;
+        const double cost = lacc.area() * double(lc) + right_area[b + 1] * double(right_cnt[b + 1]);
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = axis;
+          best_bin = b;
+        }
+      }
+    }
+    size_t mid;
+    if (best_axis < 0) {  // coincident centroids: split by position in the list
+      mid = lo + n / 2;
+    } else {
+      const float ext = cb.mx[best_axis] - cb.mn[best_axis];
+      const float scale = kBins / ext;
+      auto it = std::partition(items.begin() + lo, items.begin() + hi, [&](const Item& t) {
+        int b = int((t.c[best_axis] - cb.mn[best_axis]) * scale);
+        b = std::min(std::max(b, 0), kBins - 1);
+        return b <= best_bin;
+      });
+      mid = size_t(it - items.begin());
+      if (mid == lo || mid == hi) mid = lo + n / 2;
+    }
+    const int32_t l = build(lo, mid);
+    const int32_t r = build(mid, hi);
+    nodes[me].left = l;
+    nodes[me].right = r;
+    return me;
+  }
+};
+
+void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
+
+}  // namespace
+
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
+  WideBvh out;
+  const size_t n = leaves.size();
+  out.n_leaves = uint32_t(n);
+  out.leaves.resize(2 * n);
+  std::vector<Item> items(n);
+  for (size_t i = 0; i < n; ++i) {
+    const RefLeaf& L = leaves[i];
+    float4v lo{}, hi{};
+    for (int k = 0; k < 3; ++k) {
+      items[i].box.mn[k] = L.mn[k];
+      items[i].box.mx[k] = L.mx[k];
+      items[i].c[k] = 0.5f * (L.mn[k] + L.mx[k]);
+      lo.v[k] = L.mn[k];
+      hi.v[k] = L.mx[k];
+    }
+    std::memcpy(&lo.v[3], &L.prim_a, 4);
+    std::memcpy(&hi.v[3], &L.prim_b, 4);
+    out.leaves[2 * i] = lo;
+    out.leaves[2 * i + 1] = hi;
+    items[i].leaf = int32_t(i);
+  }
+  if (n == 0) return out;
+  Builder2 b{items, {}};
+  b.nodes.reserve(2 * n);
+  b.build(0, n);
+  const std::vector<Node2>& N = b.nodes;
+
+  // collapse to 4-wide: repeatedly open the child with the largest area
+  struct Wide {
+    int32_t child[4];
+    int count;
+  };
+  std::vector<Wide> wide;
+  std::vector<int32_t> wide_of(N.size(), -1);
+  std::vector<uint32_t> depth_of;
+  // BFS over binary nodes that become wide nodes
+  std::vector<int32_t> queue;
+  auto make_wide = [&](int32_t bn) {
+    Wide w{};
+    w.count = 0;
+    if (N[bn].leaf >= 0) {  // a single-leaf tree
+      w.child[w.count++] = bn;
+    } else {
+      w.child[w.count++] = N[bn].left;
+      w.child[w.count++] = N[bn].right;
+      while (w.count < 4) {
+        int pick = -1;
+        double best = -1.0;
+        for (int k = 0; k < w.count; ++k) {
+          const Node2& c = N[w.child[k]];
+          if (c.leaf >= 0) continue;
+          const double a = c.box.area();
+          if (a > best) {
+            best = a;
+            pick = k;
+          }
+        }
+        if (pick < 0) break;
+        const int32_t opened = w.child[pick];
+        w.child[pick] = N[opened].left;
+        w.child[w.count++] = N[opened].right;
+      }
+    }
+    wide_of[bn] = int32_t(wide.size());
+    wide.push_back(w);
+    return wide_of[bn];
+  };
+  make_wide(0);
+  depth_of.push_back(1);
+  for (size_t wi = 0; wi < wide.size(); ++wi) {
+    for (int k = 0; k < wide[wi].count; ++k) {
+      const int32_t c = wide[wi].child[k];
+      if (N[c].leaf < 0 && wide_of[c] < 0) {
+        make_wide(c);
+        depth_of.push_back(depth_of[wi] + 1);
+      }
+    }
+  }
+  out.n_nodes = uint32_t(wide.size());
+  out.nodes.resize(8 * wide.size());
+  uint32_t max_depth = 0;
+  for (size_t wi = 0; wi < wide.size(); ++wi) {
+    float4v q[8];
+    for (int k = 0; k < 8; ++k) q[k] = float4v{};
+    for (int k = 0; k < 4; ++k) {
+      int32_t ref;
+      Aabb box;  // empty by default
+      if (k < wide[wi].count) {
+        const int32_t c = wide[wi].child[k];
+        box = N[c].box;
+        ref = N[c].leaf >= 0 ? ~N[c].leaf : wide_of[c];
+      } else {
+        ref = ~0;  // never taken: the empty box fails every test
+      }
+      put4(q[0], k, box.mn[0]);
+      put4(q[1], k, box.mn[1]);
+      put4(q[2], k, box.mn[2]);
+      put4(q[3], k, box.mx[0]);
+      put4(q[4], k, box.mx[1]);
+      put4(q[5], k, box.mx[2]);
+      std::memcpy(&q[6].v[k], &ref, 4);
+    }
+    for (int k = 0; k < 8; ++k) out.nodes[8 * wi + k] = q[k];
+    max_depth = std::max(max_depth, depth_of[wi]);
+  }
+  out.depth = max_depth;
+  // near-first traversal pushes at most 3 children per wide level
+  out.max_stack = 3 * max_depth + 2;
+  return out;
+}
+
+}  // namespace zrt

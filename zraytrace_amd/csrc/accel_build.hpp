@@ -1,0 +1,27 @@
+// accel_build.hpp — wide SAH tree over the reference BVH's leaves (see accel_build.cpp).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace zrt {
+
+struct float4v {  // host-side float4 (same layout as HIP's float4)
+  float v[4];
+};
+
+// One reference leaf (bvh.zig:132-143): its exact box and its one or two
+// primitives as render.hip primitive-slot refs (-(2*slot + kind) - 1).
+struct RefLeaf {
+  float mn[3], mx[3];
+  int32_t prim_a, prim_b;
+};
+
+struct WideBvh {
+  std::vector<float4v> nodes;   // 8 per wide node, node 0 = root
+  std::vector<float4v> leaves;  // 2 per reference leaf
+  uint32_t n_nodes = 0, n_leaves = 0, depth = 0, max_stack = 0;
+};
+
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves);
+
+}  // namespace zrt

@@ -32,6 +32,7 @@
 #include <string>
 #include <vector>
 
+#include "accel_build.hpp"
 #include "bvh_build.hpp"
 #include "device_math.hpp"
 #include "zrt.hpp"
@@ -59,6 +60,8 @@ struct KArgs {
   const float4* __restrict__ nodes;
   const float4* __restrict__ prims;
   const float4* __restrict__ shade;
+  const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (8 float4 each)
+  const float4* __restrict__ wleaves;  // FAST: reference leaves (2 float4 each)
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;
   float4* __restrict__ att;            // [max_depth][n_lanes]
@@ -77,7 +80,7 @@ struct KArgs {
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
-       kNumCounters };
+       kLeaves, kNumCounters };
 constexpr int kWorkSlot = 14, kErrorSlot = 15, kScratchSlots = 16;
 
 constexpr int kBlock = 256;
@@ -359,6 +362,120 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
   }
 }
 
+// FAST: near-first over the 4-wide tree (accel_build.cpp).  Inner boxes are
+// culled with the narrowed slab test only (conservative); each reference leaf
+// reached gets the reference's own loose test (plus the narrowed one) before
+// its primitives are intersected with lower-slot tie-breaking.
+template <class StackT>
+__device__ __forceinline__ uint32_t stack_enc(int32_t ref);
+template <>
+__device__ __forceinline__ uint32_t stack_enc<uint16_t>(int32_t ref) {
+  return ref >= 0 ? uint32_t(ref) : (0x8000u | uint32_t(~ref));
+}
+template <>
+__device__ __forceinline__ uint32_t stack_enc<uint32_t>(int32_t ref) {
+  return uint32_t(ref);
+}
+template <class StackT>
+__device__ __forceinline__ int32_t stack_dec(uint32_t v);
+template <>
+__device__ __forceinline__ int32_t stack_dec<uint16_t>(uint32_t v) {
+  return (v & 0x8000u) ? ~int32_t(v & 0x7fffu) : int32_t(v);
+}
+template <>
+__device__ __forceinline__ int32_t stack_dec<uint32_t>(uint32_t v) {
+  return int32_t(v);
+}
+
+__device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
+  const bool s = kb < ka;
+  const float tk = s ? kb : ka;
+  const int tr = s ? rb : ra;
+  kb = s ? ka : kb;
+  rb = s ? ra : rb;
+  ka = tk;
+  ra = tr;
+}
+
+// narrowed slab test of child k of a wide node: entry distance or +inf on a miss
+__device__ __forceinline__ float wide_child(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                            const RayT& r, float tb) {
+  const float t_min = 0.001f;
+  float a0 = (mnx - r.ox) * r.ix, a1 = (mxx - r.ox) * r.ix;
+  float b0 = (mny - r.oy) * r.iy, b1 = (mxy - r.oy) * r.iy;
+  float c0 = (mnz - r.oz) * r.iz, c1 = (mxz - r.oz) * r.iz;
+  if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
+  if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
+  if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
+  const float en = dev::fmax_z(dev::fmax_z(dev::fmax_z(a0, t_min), dev::fmax_z(b0, t_min)), dev::fmax_z(c0, t_min));
+  const float ex = dev::fmin_z(dev::fmin_z(dev::fmin_z(a1, tb), dev::fmin_z(b1, tb)), dev::fmin_z(c1, tb));
+  return (en > ex * 1.0000153f) ? __builtin_inff() : en;
+}
+
+template <bool STATS, class StackT>
+__device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
+                                              float& best_t, int& best, uint32_t& c_nodes, uint32_t& c_leaves,
+                                              uint32_t& c_tri, uint32_t& c_sph) {
+  const int stride = kBlock;
+  const uint32_t cap = a.stack_depth;
+  uint32_t sp = 0;
+  int32_t cur = 0;  // the root wide node
+  for (;;) {
+    if (cur >= 0) {
+      const float4* q = a.wnodes + 8 * cur;
+      const float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], rf = q[6];
+      if (STATS) ++c_nodes;
+      const float tb = best_t * 1.0000153f;
+      float k0 = wide_child(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, tb);
+      float k1 = wide_child(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, tb);
+      float k2 = wide_child(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, tb);
+      float k3 = wide_child(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, tb);
+      int r0 = as_int(rf.x), r1 = as_int(rf.y), r2 = as_int(rf.z), r3 = as_int(rf.w);
+      // sort (entry, ref) ascending: 5 compare-exchanges
+      cswap(k0, r0, k1, r1);
+      cswap(k2, r2, k3, r3);
+      cswap(k0, r0, k2, r2);
+      cswap(k1, r1, k3, r3);
+      cswap(k1, r1, k2, r2);
+      const float inf = __builtin_inff();
+      if (k0 != inf) {
+        // push the farther hits (farthest first), continue with the nearest
+        if (k3 != inf) {
+          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r3);
+          ++sp;
+        }
+        if (k2 != inf) {
+          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r2);
+          ++sp;
+        }
+        if (k1 != inf) {
+          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r1);
+          ++sp;
+        }
+        if (sp > cap) {
+          atomicOr(a.error_flag, 1u);
+          sp = cap;
+        }
+        cur = r0;
+        continue;
+      }
+    } else {
+      const int leaf = ~cur;
+      const float4 lo = a.wleaves[2 * leaf], hi = a.wleaves[2 * leaf + 1];
+      if (STATS) ++c_leaves;
+      float e;
+      if (box_test<true>(lo, hi, r, best_t * 1.0000153f, &e)) {
+        const int pa = as_int(lo.w), pb = as_int(hi.w);
+        prim_test<true, STATS>(a.prims, pa, r, best_t, best, c_tri, c_sph);
+        if (pb != pa) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph);
+      }
+    }
+    if (sp == 0) return;
+    --sp;
+    cur = stack_dec<StackT>((uint32_t)stk[sp * stride]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // shading
 // ---------------------------------------------------------------------------
@@ -443,11 +560,15 @@ constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 
 // StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
 // more blocks fit per CU), uint32_t otherwise.
-template <int MODE /*0 list, 1 BVH fast, 2 BVH reference*/, int PRNG, bool STATS, class StackT>
+template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
 #ifndef ZRT_WAVES_PER_SIMD
-#define ZRT_WAVES_PER_SIMD 8  // A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
+#define ZRT_WAVES_PER_SIMD 8  // binary/reference/list; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
 #endif
-__global__ void __launch_bounds__(kBlock, ZRT_WAVES_PER_SIMD) render_kernel(const KArgs a) {
+#ifndef ZRT_WAVES_WIDE
+#define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B: w4 12.9, w5 13.9, w6 13.4 Gray/s
+#endif
+__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
+    render_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
   const int lane = (int)__lane_id();
@@ -462,7 +583,7 @@ __global__ void __launch_bounds__(kBlock, ZRT_WAVES_PER_SIMD) render_kernel(cons
   Rng<PRNG> rng;
   rng.init(0);
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
-  uint32_t c_shade = 0, c_tex = 0;
+  uint32_t c_shade = 0, c_tex = 0, c_leaves = 0;
   const uint32_t per_tile = 64u * a.n_chunks;
 
   for (;;) {
@@ -542,6 +663,8 @@ __global__ void __launch_bounds__(kBlock, ZRT_WAVES_PER_SIMD) render_kernel(cons
             sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
           }
         }
+      } else if (MODE == 3) {
+        traverse_wide<STATS>(a, r, stk, best_t, best, c_nodes, c_leaves, c_tri, c_sph);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
@@ -669,6 +792,7 @@ __global__ void __launch_bounds__(kBlock, ZRT_WAVES_PER_SIMD) render_kernel(cons
     wave_add_u64(&a.counters[kSphereTests], c_sph);
     wave_add_u64(&a.counters[kShades], c_shade);
     wave_add_u64(&a.counters[kTexels], c_tex);
+    wave_add_u64(&a.counters[kLeaves], c_leaves);
   }
 }
 
@@ -847,7 +971,7 @@ int validate_params(const zrt_params* p) {
     return fail(ZRT_E_UNSUPPORTED,
                 "the single sequential reference stream cannot be split across GPU lanes; use ZRT_RNG_COUNTER");
   if (p->prng > ZRT_PRNG_XOSHIRO256) return fail(ZRT_E_INVALID, "unknown prng");
-  if (p->traversal > ZRT_TRAVERSAL_REFERENCE) return fail(ZRT_E_INVALID, "unknown traversal");
+  if (p->traversal > ZRT_TRAVERSAL_BINARY) return fail(ZRT_E_INVALID, "unknown traversal");
   if (p->world_size == 0 || p->rank >= p->world_size) return fail(ZRT_E_INVALID, "rank must be < world_size");
   if (p->sample_chunk > 65535) return fail(ZRT_E_INVALID, "sample_chunk must be <= 65535");
   return ZRT_OK;
@@ -876,6 +1000,8 @@ struct zrt_ctx {
   hipStream_t stream = nullptr;
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
+  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0;
+  zrt::DevBuf<float4> wnodes, wleaves;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
@@ -888,6 +1014,7 @@ struct zrt_ctx {
   // last launch
   uint32_t last_pixels = 0, last_spp = 0, launched = 0;
   bool last_stats = false;
+  int last_mode = 0;
   int cu_count = 0;
   ~zrt_ctx() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -921,10 +1048,21 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
       const int32_t kind = s->prims[prim].kind == ZRT_PRIM_TRIANGLE ? 1 : 0;
       return -(2 * prim_slot[prim] + kind) - 1;
     };
+    std::vector<RefLeaf> leaves;
     for (size_t i = 0; i < bvh.nodes.size(); ++i) {  // pre-order == reference DFS order
       const BuildNode& b = bvh.nodes[i];
       const int32_t l = ref_of(b.left);
       const int32_t r = ref_of(b.right);
+      if (b.left < 0) {  // a reference leaf: its box and its primitive refs
+        RefLeaf L;
+        for (int k = 0; k < 3; ++k) {
+          L.mn[k] = b.mn[k];
+          L.mx[k] = b.mx[k];
+        }
+        L.prim_a = l;
+        L.prim_b = r;
+        leaves.push_back(L);
+      }
       float4 lo, hi;
       lo.x = b.mn[0]; lo.y = b.mn[1]; lo.z = b.mn[2];
       hi.x = b.mx[0]; hi.y = b.mx[1]; hi.z = b.mx[2];
@@ -934,6 +1072,15 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
       nodes[2 * i + 1] = hi;
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
+    const WideBvh wide = build_wide_bvh(leaves);
+    std::vector<float4> wn(wide.nodes.size()), wl(wide.leaves.size());
+    std::memcpy(wn.data(), wide.nodes.data(), wn.size() * sizeof(float4));
+    std::memcpy(wl.data(), wide.leaves.data(), wl.size() * sizeof(float4));
+    c->wnodes.upload(wn);
+    c->wleaves.upload(wl);
+    c->n_wide = wide.n_nodes;
+    c->n_leaves = wide.n_leaves;
+    c->wide_stack = wide.max_stack;
   } else {
     for (uint32_t i = 0; i < n; ++i) slot_to_prim.push_back(i);
   }
@@ -1023,6 +1170,7 @@ template <int PRNG, bool STATS>
 void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 0) return kernel_ptr<0, PRNG, STATS, uint16_t>();  // list mode: no stack
   if (mode == 1) return stk16 ? kernel_ptr<1, PRNG, STATS, uint16_t>() : kernel_ptr<1, PRNG, STATS, uint32_t>();
+  if (mode == 3) return stk16 ? kernel_ptr<3, PRNG, STATS, uint16_t>() : kernel_ptr<3, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
 void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
@@ -1110,11 +1258,14 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const zrt::Geometry g = zrt::geometry(p);
     const uint32_t my_tiles = zrt::rank_tiles(g, p->rank, p->world_size);
-    const int mode = !c->use_bvh ? 0 : (p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2 : 1);
+    const int mode = !c->use_bvh ? 0
+                     : p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2
+                     : p->traversal == ZRT_TRAVERSAL_BINARY ? 1 : 3;
     const bool diag = (p->flags & ZRT_FLAG_STATS) != 0;
-    const bool stk16 = c->n_nodes < 65536;
+    const bool stk16 = mode == 3 ? (c->n_wide < 32768 && c->n_leaves < 32768) : c->n_nodes < 65536;
+    const uint32_t stack_depth = mode == 3 ? c->wide_stack : c->stack_depth;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
-    const size_t lds = size_t(c->stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
+    const size_t lds = size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
@@ -1165,7 +1316,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.world = p->world_size;
     a.total_work = work;
     a.n_list = c->use_bvh ? 0 : c->n_prims;
-    a.stack_depth = c->stack_depth;
+    a.stack_depth = stack_depth;
+    a.wnodes = c->wnodes.p;
+    a.wleaves = c->wleaves.p;
     a.n_lanes = uint32_t(n_lanes);
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
     a.chunk = chunk;
@@ -1195,6 +1348,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_pixels = uint32_t(pixels);
     c->last_spp = p->samples_per_pixel;
     c->last_stats = diag;
+    c->last_mode = mode;
     c->launched = 1;
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
@@ -1224,6 +1378,9 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->sphere_tests = h[zrt::kSphereTests];
     out->shade_fetches = h[zrt::kShades];
     out->texel_fetches = h[zrt::kTexels];
+    out->leaf_visits = h[zrt::kLeaves];
+    out->node_bytes = c->last_mode == 3 ? 128 : 32;
+    out->wide_nodes = c->n_wide;
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
     out->preprocess_ms = c->preprocess_ms;
