@@ -202,13 +202,17 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
   if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
   if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
-  const float an = dev::fmax_z(a0, t_min), ax = dev::fmin_z(a1, t_max);
-  const float bn = dev::fmax_z(b0, t_min), bx = dev::fmin_z(b1, t_max);
-  const float cn = dev::fmax_z(c0, t_min), cx = dev::fmin_z(c1, t_max);
+  // math.max(t0, t_min) / math.min(t1, t_max) are `x > y ? x : y` / `x < y ? x : y`.
+  // With a non-NaN second operand (t_min, t_max never are) these equal IEEE
+  // maxNum / minNum (v_max_f32 / v_min_f32) for every NaN first operand, and
+  // differ only in the sign of a zero result, which no comparison below sees.
+  const float an = __builtin_fmaxf(a0, t_min), ax = __builtin_fminf(a1, t_max);
+  const float bn = __builtin_fmaxf(b0, t_min), bx = __builtin_fminf(b1, t_max);
+  const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, t_max);
   bool ok = (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) for every axis
   if (FAST) {
-    const float en = dev::fmax_z(dev::fmax_z(an, bn), cn);
-    const float ex = dev::fmin_z(dev::fmin_z(ax, bx), cx);
+    const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
+    const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
     ok = ok && !(en > ex * 1.0000153f);
     *entry = en;
   }
@@ -407,8 +411,10 @@ __device__ __forceinline__ float wide_child(float mnx, float mny, float mnz, flo
   if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
   if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
   if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
-  const float en = dev::fmax_z(dev::fmax_z(dev::fmax_z(a0, t_min), dev::fmax_z(b0, t_min)), dev::fmax_z(c0, t_min));
-  const float ex = dev::fmin_z(dev::fmin_z(dev::fmin_z(a1, tb), dev::fmin_z(b1, tb)), dev::fmin_z(c1, tb));
+  // maxNum/minNum ignore a NaN slab bound ((bound - o) * inf with bound == o):
+  // that axis then constrains nothing, as in the reference's test.
+  const float en = __builtin_fmaxf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(c0, t_min));
+  const float ex = __builtin_fminf(__builtin_fminf(a1, b1), __builtin_fminf(c1, tb));
   return (en > ex * 1.0000153f) ? __builtin_inff() : en;
 }
 
@@ -565,7 +571,7 @@ template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int
 #define ZRT_WAVES_PER_SIMD 8  // binary/reference/list; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
 #endif
 #ifndef ZRT_WAVES_WIDE
-#define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B: w4 12.9, w5 13.9, w6 13.4 Gray/s
+#define ZRT_WAVES_WIDE 6      // FAST (wide tree) kernel; A/B: w4 15.2, w5 16.6, w6 17.3, w7 17.3 Gray/s
 #endif
 __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
