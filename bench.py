@@ -34,13 +34,13 @@ def log(*a):
 
 def algorithmic_bytes(st, n_work_units, n_pixels):
     """Bytes the sampling loop must touch per launch:
-    per node record read (32 B binary/reference node, 128 B wide node), 32 B
-    per reference leaf opened (wide traversal), 48 B per triangle test, 16 B per sphere test,
+    per node record read (32 B binary/reference node; 128 B wide node, which
+    also carries its leaf children's boxes), 48 B per triangle test, 16 B per sphere test,
     64 B per shaded hit (16 B shade record + 48 B material), 12 B per texel,
     32 B per scatter (attenuation pushed + read back), 16 B per chunk sum
     written and read, 12 B per output pixel."""
     tri = st["prim_tests"] - st["sphere_tests"]
-    return (st["node_bytes"] * st["node_visits"] + 32 * st["leaf_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
+    return (st["node_bytes"] * st["node_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
             + 12 * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 

@@ -180,7 +180,7 @@ typedef struct zrt_stats {
   uint64_t sphere_tests;  /* ... of which spheres */
   uint64_t shade_fetches; /* closest hits shaded (hit record + material reads) */
   uint64_t texel_fetches; /* image-texture lookups */
-  uint64_t leaf_visits;   /* FAST traversal: reference leaves opened (node_visits = wide nodes) */
+  uint64_t leaf_visits;   /* FAST traversal: reference leaf boxes tested (node_visits = wide nodes) */
   double preprocess_ms;   /* BVH build + flatten (raytrace.zig:150) */
   double upload_ms;
   double render_ms;       /* kernel time (HIP events) */
@@ -245,6 +245,11 @@ int zrt_ctx_assemble(zrt_ctx* ctx, const zrt_params* params,
 
 /* Counters of the last zrt_ctx_render_tiles (synchronises the ctx stream). */
 int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
+
+/* Raw device counter slots of the last launch (diagnostics; n <= 24):
+ * [0..9] progress/traffic counters, [14] work counter, [15] error flag,
+ * [16..20] per-section cycle sums of ZRT_PROFILE builds. */
+int zrt_ctx_debug_counters(zrt_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* Duration in ms of the last zrt_ctx_render_tiles' kernel (HIP events on the
  * launch stream; synchronises). */

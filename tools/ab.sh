@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B build variants on the GPU box: interleaved rounds of bench.py per variant.
-# usage: bash tools/ab.sh <tag> <rounds> <variant>... [-- bench args]
+# usage: bash tools/ab.sh <tag> <rounds> <variant>[@chunk]... [-- bench args]
 set -o pipefail
 TAG=$1; ROUNDS=$2; shift 2
 VARS=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do VARS+=("$1"); shift; done
@@ -8,9 +8,10 @@ VARS=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do VARS+=("$1"); shift; done
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG; mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
-  for v in "${VARS[@]}"; do
+  for spec in "${VARS[@]}"; do
+    v=${spec%%@*}; EXTRA_ARGS=(); [ "$spec" != "$v" ] && EXTRA_ARGS=(--chunk ${spec#*@})
     if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/build/variants/$v/libzrt.so; fi
-    ZRT_LIB=$LIB timeout -k 10 300 python $R/bench.py --no-cpu-baseline "$@" > $OUT/$v.$r.json 2> $OUT/$v.$r.err || { echo "variant $v failed"; tail -5 $OUT/$v.$r.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('$OUT/$v.$r.json')); print('$v', $r, d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['roofline']['per_ray'])"
+    ZRT_LIB=$LIB timeout -k 10 300 python $R/bench.py --no-cpu-baseline "$@" "${EXTRA_ARGS[@]}" > $OUT/$spec.$r.json 2> $OUT/$spec.$r.err || { echo "variant $v failed"; tail -5 $OUT/$spec.$r.err; exit 1; }
+    python -c "import json,sys; d=json.load(open('$OUT/$spec.$r.json')); print('$spec', $r, d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['roofline']['per_ray'])"
   done
 done

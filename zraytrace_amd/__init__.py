@@ -148,6 +148,11 @@ class RenderContext:
         check(lib().zrt_ctx_stats(self._h, C.byref(st)))
         return st.as_dict()
 
+    def debug_counters(self, n: int = 24):
+        out = (C.c_uint64 * n)()
+        check(lib().zrt_ctx_debug_counters(self._h, out, n))
+        return list(out)
+
     def kernel_ms(self) -> float:
         ms = C.c_double()
         check(lib().zrt_ctx_last_kernel_ms(self._h, C.byref(ms)))

@@ -117,6 +117,7 @@ SIGNATURES = [
     ("zrt_ctx_assemble", C.c_int, [_P, C.POINTER(Params), _P, _P, _P]),
     ("zrt_ctx_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("zrt_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
+    ("zrt_ctx_debug_counters", C.c_int, [_P, C.POINTER(C.c_uint64), C.c_uint32]),
     ("zrt_scene_load", C.c_int, [C.c_uint32, C.c_char_p, C.POINTER(_P), C.POINTER(Camera)]),
     ("zrt_scene_view", C.POINTER(Scene), [_P]),
     ("zrt_scene_free", None, [_P]),
@@ -160,6 +161,8 @@ def load(path: str = LIB_PATH):
             "(python -c 'import __graft_entry__ as g; g.build()'); there is no fallback path")
     lib = C.CDLL(path)
     for name, restype, argtypes in SIGNATURES:
+        if path != os.path.join(HERE, "libzrt.so") and not hasattr(lib, name):
+            continue  # an older A/B build variant (ZRT_LIB) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes

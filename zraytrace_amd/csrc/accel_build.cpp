@@ -22,11 +22,12 @@
 // Device layout (filled here, read by render.hip):
 //   wide node = 8 x float4 (128 B, one cache line):
 //     {min.x of children 0..3}, {min.y}, {min.z}, {max.x}, {max.y}, {max.z},
-//     {child refs (int bits)}, {unused}
-//     child ref >= 0: wide node index; ref < 0: reference leaf ~ref;
-//     an empty child slot has an empty box (min = +inf, max = -inf).
-//   reference leaf = 2 x float4 (32 B): {min.xyz, prim ref a}, {max.xyz, prim ref b}
-//     with the primitive-slot refs of render.hip (b == a for a one-primitive leaf).
+//     {ref a of children 0..3}, {ref b of children 0..3}   (int bits)
+//     inner child: ref a = wide node index (>= 0);
+//     leaf child:  the box IS the reference leaf's box (bit for bit) and
+//                  ref a / ref b are its one or two primitive-slot refs of
+//                  render.hip (< 0; b == a for a one-primitive leaf);
+//     empty slot:  an empty box (min = +inf, max = -inf), never entered.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -160,22 +161,14 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
   WideBvh out;
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
-  out.leaves.resize(2 * n);
   std::vector<Item> items(n);
   for (size_t i = 0; i < n; ++i) {
     const RefLeaf& L = leaves[i];
-    float4v lo{}, hi{};
     for (int k = 0; k < 3; ++k) {
       items[i].box.mn[k] = L.mn[k];
       items[i].box.mx[k] = L.mx[k];
       items[i].c[k] = 0.5f * (L.mn[k] + L.mx[k]);
-      lo.v[k] = L.mn[k];
-      hi.v[k] = L.mx[k];
     }
-    std::memcpy(&lo.v[3], &L.prim_a, 4);
-    std::memcpy(&hi.v[3], &L.prim_b, 4);
-    out.leaves[2 * i] = lo;
-    out.leaves[2 * i + 1] = hi;
     items[i].leaf = int32_t(i);
   }
   if (n == 0) return out;
@@ -242,14 +235,18 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
     float4v q[8];
     for (int k = 0; k < 8; ++k) q[k] = float4v{};
     for (int k = 0; k < 4; ++k) {
-      int32_t ref;
-      Aabb box;  // empty by default
+      int32_t ref = -1, ref_b = -1;  // empty slot: never entered (empty box)
+      Aabb box;                      // empty by default
       if (k < wide[wi].count) {
         const int32_t c = wide[wi].child[k];
         box = N[c].box;
-        ref = N[c].leaf >= 0 ? ~N[c].leaf : wide_of[c];
-      } else {
-        ref = ~0;  // never taken: the empty box fails every test
+        if (N[c].leaf >= 0) {
+          ref = leaves[size_t(N[c].leaf)].prim_a;
+          ref_b = leaves[size_t(N[c].leaf)].prim_b;
+        } else {
+          ref = wide_of[c];
+          ref_b = 0;
+        }
       }
       put4(q[0], k, box.mn[0]);
       put4(q[1], k, box.mn[1]);
@@ -258,12 +255,13 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
       put4(q[4], k, box.mx[1]);
       put4(q[5], k, box.mx[2]);
       std::memcpy(&q[6].v[k], &ref, 4);
+      std::memcpy(&q[7].v[k], &ref_b, 4);
     }
     for (int k = 0; k < 8; ++k) out.nodes[8 * wi + k] = q[k];
     max_depth = std::max(max_depth, depth_of[wi]);
   }
   out.depth = max_depth;
-  // near-first traversal pushes at most 3 children per wide level
+  // near-first traversal pushes at most 3 inner children per wide level
   out.max_stack = 3 * max_depth + 2;
   return out;
 }

@@ -18,7 +18,6 @@ struct RefLeaf {
 
 struct WideBvh {
   std::vector<float4v> nodes;   // 8 per wide node, node 0 = root
-  std::vector<float4v> leaves;  // 2 per reference leaf
   uint32_t n_nodes = 0, n_leaves = 0, depth = 0, max_stack = 0;
 };
 

@@ -61,7 +61,6 @@ struct KArgs {
   const float4* __restrict__ prims;
   const float4* __restrict__ shade;
   const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (8 float4 each)
-  const float4* __restrict__ wleaves;  // FAST: reference leaves (2 float4 each)
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;
   float4* __restrict__ att;            // [max_depth][n_lanes]
@@ -74,16 +73,39 @@ struct KArgs {
   uint32_t width, height, xbound, spp, max_depth;
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
-  uint32_t chunk, n_chunks;
+  uint32_t chunk, n_chunks, unit_chunks, n_groups;
   unsigned long long seed_mix;
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
        kLeaves, kNumCounters };
-constexpr int kWorkSlot = 14, kErrorSlot = 15, kScratchSlots = 16;
+constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 24;
+
+// ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
+// cycle sums per loop section into counters[kProfSlot + section].
+#ifndef ZRT_PROFILE
+#define ZRT_PROFILE 0
+#endif
+__device__ __forceinline__ uint64_t prof_stamp() {
+  uint64_t t = 0;
+#if ZRT_PROFILE
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+  return t;
+}
 
 constexpr int kBlock = 256;
+#ifndef ZRT_UNIT_CHUNKS
+#define ZRT_UNIT_CHUNKS 1  // chunks of one pixel per work unit (a unit = 8x8 tile x this many chunks)
+#endif
+#ifndef ZRT_UNIT_RING
+#define ZRT_UNIT_RING 4    // units a wave keeps in flight
+#endif
+constexpr uint32_t kUnitRing = ZRT_UNIT_RING;
+constexpr uint32_t kRingBytes = (kBlock / 64) * kUnitRing * 4;
 
 // ---------------------------------------------------------------------------
 // RNG: std.rand DefaultPrng restated per (pixel, sample)
@@ -366,29 +388,33 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
   }
 }
 
-// FAST: near-first over the 4-wide tree (accel_build.cpp).  Inner boxes are
-// culled with the narrowed slab test only (conservative); each reference leaf
-// reached gets the reference's own loose test (plus the narrowed one) before
-// its primitives are intersected with lower-slot tie-breaking.
-template <class StackT>
-__device__ __forceinline__ uint32_t stack_enc(int32_t ref);
-template <>
-__device__ __forceinline__ uint32_t stack_enc<uint16_t>(int32_t ref) {
-  return ref >= 0 ? uint32_t(ref) : (0x8000u | uint32_t(~ref));
-}
-template <>
-__device__ __forceinline__ uint32_t stack_enc<uint32_t>(int32_t ref) {
-  return uint32_t(ref);
-}
-template <class StackT>
-__device__ __forceinline__ int32_t stack_dec(uint32_t v);
-template <>
-__device__ __forceinline__ int32_t stack_dec<uint16_t>(uint32_t v) {
-  return (v & 0x8000u) ? ~int32_t(v & 0x7fffu) : int32_t(v);
-}
-template <>
-__device__ __forceinline__ int32_t stack_dec<uint32_t>(uint32_t v) {
-  return int32_t(v);
+// Slab test of child slot k of a wide node: entry distance, or +inf on a miss.
+// Every slot gets the narrowed test (entry > exit * (1 + 2^-16) culls; it never
+// rejects a box holding a hit closer than best_t).  A leaf slot additionally
+// gets the reference's own loose test (aabb.zig:109-127: each axis on its own
+// against [t_min, t_max]) - its box is the reference leaf's box bit for bit.
+__device__ __forceinline__ float wide_slot(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                           const RayT& r, float tb, bool leaf) {
+  const float t_min = 0.001f;
+  float a0 = (mnx - r.ox) * r.ix, a1 = (mxx - r.ox) * r.ix;
+  float b0 = (mny - r.oy) * r.iy, b1 = (mxy - r.oy) * r.iy;
+  float c0 = (mnz - r.oz) * r.iz, c1 = (mxz - r.oz) * r.iz;
+  if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
+  if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
+  if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
+  // math.max(t0, t_min) / math.min(t1, t_max) are `x > y ? x : y` / `x < y ? x : y`;
+  // with a non-NaN second operand these equal maxNum / minNum for every first
+  // operand (a NaN slab bound, (bound - o) * inf with bound == o, then
+  // constrains nothing, as in the reference) up to the sign of a zero result,
+  // which no comparison below sees.
+  const float an = __builtin_fmaxf(a0, t_min), ax = __builtin_fminf(a1, tb);
+  const float bn = __builtin_fmaxf(b0, t_min), bx = __builtin_fminf(b1, tb);
+  const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, tb);
+  const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
+  const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
+  bool ok = !(en > ex * 1.0000153f);
+  if (leaf) ok = ok && (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) per axis
+  return ok ? en : __builtin_inff();
 }
 
 __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
@@ -401,84 +427,89 @@ __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   ra = tr;
 }
 
-// narrowed slab test of child k of a wide node: entry distance or +inf on a miss
-__device__ __forceinline__ float wide_child(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                                            const RayT& r, float tb) {
-  const float t_min = 0.001f;
-  float a0 = (mnx - r.ox) * r.ix, a1 = (mxx - r.ox) * r.ix;
-  float b0 = (mny - r.oy) * r.iy, b1 = (mxy - r.oy) * r.iy;
-  float c0 = (mnz - r.oz) * r.iz, c1 = (mxz - r.oz) * r.iz;
-  if (r.ix < 0.0f) { const float t = a0; a0 = a1; a1 = t; }
-  if (r.iy < 0.0f) { const float t = b0; b0 = b1; b1 = t; }
-  if (r.iz < 0.0f) { const float t = c0; c0 = c1; c1 = t; }
-  // maxNum/minNum ignore a NaN slab bound ((bound - o) * inf with bound == o):
-  // that axis then constrains nothing, as in the reference's test.
-  const float en = __builtin_fmaxf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(c0, t_min));
-  const float ex = __builtin_fminf(__builtin_fminf(a1, b1), __builtin_fminf(c1, tb));
-  return (en > ex * 1.0000153f) ? __builtin_inff() : en;
-}
-
+// FAST: near-first over the 4-wide tree (accel_build.cpp).  All four slots of
+// a node are tested against the t_max at node entry (a leaf passing with a
+// t_max >= the current one is a superset of what the reference opens, and
+// every primitive test still uses the current best with lower-slot
+// tie-breaking); leaf slots are intersected in place, inner slots are sorted
+// by entry distance, the farther ones pushed.
 template <bool STATS, class StackT>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                               float& best_t, int& best, uint32_t& c_nodes, uint32_t& c_leaves,
                                               uint32_t& c_tri, uint32_t& c_sph) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;
+  const float inf = __builtin_inff();
   uint32_t sp = 0;
   int32_t cur = 0;  // the root wide node
   for (;;) {
-    if (cur >= 0) {
-      const float4* q = a.wnodes + 8 * cur;
-      const float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], rf = q[6];
-      if (STATS) ++c_nodes;
+    const float4* q = a.wnodes + 8 * cur;
+    float k0, k1, k2, k3;
+    int r0, r1, r2, r3;
+    {
+      const float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], ra = q[6];
+      r0 = as_int(ra.x);
+      r1 = as_int(ra.y);
+      r2 = as_int(ra.z);
+      r3 = as_int(ra.w);
       const float tb = best_t * 1.0000153f;
-      float k0 = wide_child(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, tb);
-      float k1 = wide_child(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, tb);
-      float k2 = wide_child(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, tb);
-      float k3 = wide_child(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, tb);
-      int r0 = as_int(rf.x), r1 = as_int(rf.y), r2 = as_int(rf.z), r3 = as_int(rf.w);
-      // sort (entry, ref) ascending: 5 compare-exchanges
-      cswap(k0, r0, k1, r1);
-      cswap(k2, r2, k3, r3);
-      cswap(k0, r0, k2, r2);
-      cswap(k1, r1, k3, r3);
-      cswap(k1, r1, k2, r2);
-      const float inf = __builtin_inff();
-      if (k0 != inf) {
-        // push the farther hits (farthest first), continue with the nearest
-        if (k3 != inf) {
-          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r3);
-          ++sp;
-        }
-        if (k2 != inf) {
-          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r2);
-          ++sp;
-        }
-        if (k1 != inf) {
-          if (sp < cap) stk[sp * stride] = (StackT)stack_enc<StackT>(r1);
-          ++sp;
-        }
-        if (sp > cap) {
-          atomicOr(a.error_flag, 1u);
-          sp = cap;
-        }
-        cur = r0;
-        continue;
+      k0 = wide_slot(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, tb, r0 < 0);
+      k1 = wide_slot(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, tb, r1 < 0);
+      k2 = wide_slot(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, tb, r2 < 0);
+      k3 = wide_slot(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, tb, r3 < 0);
+    }
+    if (STATS) {
+      ++c_nodes;
+      c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
+    }
+    if ((r0 < 0 && k0 != inf) || (r1 < 0 && k1 != inf) || (r2 < 0 && k2 != inf) || (r3 < 0 && k3 != inf)) {
+      const float4 rb = q[7];
+#define ZRT_WIDE_LEAF(K, RB)                                                        \
+  if (r##K < 0 && k##K != inf) {                                                    \
+    const int pb = as_int(RB);                                                      \
+    prim_test<true, STATS>(a.prims, r##K, r, best_t, best, c_tri, c_sph);           \
+    if (pb != r##K) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
+  }
+      ZRT_WIDE_LEAF(0, rb.x)
+      ZRT_WIDE_LEAF(1, rb.y)
+      ZRT_WIDE_LEAF(2, rb.z)
+      ZRT_WIDE_LEAF(3, rb.w)
+#undef ZRT_WIDE_LEAF
+    }
+    k0 = r0 < 0 ? inf : k0;
+    k1 = r1 < 0 ? inf : k1;
+    k2 = r2 < 0 ? inf : k2;
+    k3 = r3 < 0 ? inf : k3;
+    // sort (entry, ref) ascending: 5 compare-exchanges
+    cswap(k0, r0, k1, r1);
+    cswap(k2, r2, k3, r3);
+    cswap(k0, r0, k2, r2);
+    cswap(k1, r1, k3, r3);
+    cswap(k1, r1, k2, r2);
+    if (k0 != inf) {
+      // push the farther inner children (farthest first), continue with the nearest
+      if (k3 != inf) {
+        if (sp < cap) stk[sp * stride] = (StackT)r3;
+        ++sp;
       }
-    } else {
-      const int leaf = ~cur;
-      const float4 lo = a.wleaves[2 * leaf], hi = a.wleaves[2 * leaf + 1];
-      if (STATS) ++c_leaves;
-      float e;
-      if (box_test<true>(lo, hi, r, best_t * 1.0000153f, &e)) {
-        const int pa = as_int(lo.w), pb = as_int(hi.w);
-        prim_test<true, STATS>(a.prims, pa, r, best_t, best, c_tri, c_sph);
-        if (pb != pa) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph);
+      if (k2 != inf) {
+        if (sp < cap) stk[sp * stride] = (StackT)r2;
+        ++sp;
       }
+      if (k1 != inf) {
+        if (sp < cap) stk[sp * stride] = (StackT)r1;
+        ++sp;
+      }
+      if (sp > cap) {
+        atomicOr(a.error_flag, 1u);
+        sp = cap;
+      }
+      cur = r0;
+      continue;
     }
     if (sp == 0) return;
     --sp;
-    cur = stack_dec<StackT>((uint32_t)stk[sp * stride]);
+    cur = (int32_t)stk[sp * stride];
   }
 }
 
@@ -576,12 +607,16 @@ template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int
 __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
+  // LDS: [per-wave unit ring: kWavesPerBlock x kUnitRing u32][traversal stack]
+  uint32_t* ring = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kUnitRing;
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw + kRingBytes) + threadIdx.x;
   const int lane = (int)__lane_id();
   const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
 
   bool need = true, done = false, in_sample = false;
-  uint32_t work = 0, px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
+  uint32_t px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
+  uint32_t seq = 0, chunk_j = 0, chunk_end = 0;  // this lane's place in the wave's unit sequence
+  uint32_t acquired = 0;                          // units the wave has taken (wave-uniform)
   uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -590,43 +625,47 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
   rng.init(0);
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0;
-  const uint32_t per_tile = 64u * a.n_chunks;
 
+  uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
   for (;;) {
-    // ---- refill lanes whose pixel is finished: one atomic per wave
-    const bool want = need && !done;
-    const unsigned long long m = __ballot(want);
-    if (m) {
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(a.work_counter, (uint32_t)__popcll(m));
-      base = __shfl(base, leader);
-      if (want) {
-        work = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (work >= a.total_work) {
-          done = true;
+    uint64_t t0 = prof_stamp();
+    // ---- work: the WAVE takes units (local tile lt, group of unit_chunks
+    // chunks) from the global counter, one atomic per unit; lane p works on
+    // pixel p of the wave's units in sequence.  The 64 lanes of a wave so
+    // stay on one or two 8x8 tiles (coherent camera rays) while each lane
+    // still moves on by itself.  The wave keeps its last kUnitRing units in
+    // LDS and takes a new one only when no lane still works kUnitRing behind.
+    const bool want_new = need && !done && seq == acquired;
+    if (__ballot(want_new) != 0ull && __ballot(!done && seq + kUnitRing <= acquired) == 0ull) {
+      if (lane == 0) ring[acquired % kUnitRing] = atomicAdd(a.work_counter, 1u);
+      ++acquired;
+    }
+    if (need && !done && seq < acquired) {
+      const uint32_t u = ring[seq % kUnitRing];
+      if (u >= a.total_work) {
+        done = true;  // the counter is exhausted; later units are too
+      } else {
+        const uint32_t lt = u / a.n_groups, g = u - lt * a.n_groups;
+        const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
+        px = (t % a.tiles_x) * 8u + ((uint32_t)lane & 7u);
+        py = (t / a.tiles_x) * 8u + ((uint32_t)lane >> 3);
+        if (px < a.xbound && py < a.height) {  // else: finalize writes black
+          need = false;
+          chunk_j = g * a.unit_chunks;
+          chunk_end = min(chunk_j + a.unit_chunks, a.n_chunks);
+          slot = (lt * 64u + (uint32_t)lane) * a.n_chunks + chunk_j;
+          sample = chunk_j * a.chunk;
+          sample_end = min(sample + a.chunk, a.spp);
+          acc_r = acc_g = acc_b = 0.0f;
+          in_sample = false;
+          offset = (uint64_t)py * a.width + px;
         } else {
-          // work = (local tile lt, chunk j, pixel p); local tile lt of this
-          // rank is global tile lt*world + rank; the 64 pixels of one tile
-          // and chunk are consecutive, so a wave starts on one 8x8 tile.
-          const uint32_t lt = work / per_tile, rem = work - lt * per_tile;
-          const uint32_t j = rem >> 6, p = rem & 63u;
-          const uint32_t t = lt * a.world + a.rank;
-          px = (t % a.tiles_x) * 8u + (p & 7u);
-          py = (t / a.tiles_x) * 8u + (p >> 3);
-          if (px < a.xbound && py < a.height) {  // else: finalize writes black
-            need = false;
-            slot = (lt * 64u + p) * a.n_chunks + j;
-            sample = j * a.chunk;
-            sample_end = min(sample + a.chunk, a.spp);
-            acc_r = acc_g = acc_b = 0.0f;
-            in_sample = false;
-            offset = (uint64_t)py * a.width + px;
-          }
+          ++seq;
         }
       }
     }
     if (__ballot(!done) == 0ull) break;
+    if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[0] += t - t0; t0 = t; }
     if (done || need) continue;
 
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
@@ -643,6 +682,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       nb = 0;
       in_sample = true;
     }
+    if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[1] += t - t0; t0 = t; }
 
     // ---- one rayColor step (raytrace.zig:62-100)
     bool path_end = false, sky = false;
@@ -674,6 +714,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
+      if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
       if (best < 0) {
         ++c_bg;
         L = background(d);
@@ -768,6 +809,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       }
     }
 
+    if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
     if (path_end) {
       // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
       V3 col = L;
@@ -783,10 +825,20 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       in_sample = false;
       if (++sample == sample_end) {  // chunk done: its sequential sum
         a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
-        need = true;
+        if (++chunk_j < chunk_end) {  // next chunk of this unit
+          ++slot;
+          sample_end = min(sample + a.chunk, a.spp);
+          acc_r = acc_g = acc_b = 0.0f;
+        } else {
+          ++seq;
+          need = true;
+        }
       }
     }
+    if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
   }
+  if (ZRT_PROFILE && lane == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&a.counters[kProfSlot + k], (unsigned long long)pf[k]);
 
   wave_add_u64(&a.counters[kDepthHits], c_depth);
   wave_add_u64(&a.counters[kReflections], c_refl);
@@ -1007,7 +1059,7 @@ struct zrt_ctx {
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
   uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0;
-  zrt::DevBuf<float4> wnodes, wleaves;
+  zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
@@ -1079,11 +1131,9 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
     const WideBvh wide = build_wide_bvh(leaves);
-    std::vector<float4> wn(wide.nodes.size()), wl(wide.leaves.size());
+    std::vector<float4> wn(wide.nodes.size());
     std::memcpy(wn.data(), wide.nodes.data(), wn.size() * sizeof(float4));
-    std::memcpy(wl.data(), wide.leaves.data(), wl.size() * sizeof(float4));
     c->wnodes.upload(wn);
-    c->wleaves.upload(wl);
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
     c->wide_stack = wide.max_stack;
@@ -1268,20 +1318,25 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                      : p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2
                      : p->traversal == ZRT_TRAVERSAL_BINARY ? 1 : 3;
     const bool diag = (p->flags & ZRT_FLAG_STATS) != 0;
-    const bool stk16 = mode == 3 ? (c->n_wide < 32768 && c->n_leaves < 32768) : c->n_nodes < 65536;
+    const bool stk16 = mode == 3 ? c->n_wide < 65536 : c->n_nodes < 65536;
     const uint32_t stack_depth = mode == 3 ? c->wide_stack : c->stack_depth;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
-    const size_t lds = size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
+    const size_t lds =
+        zrt::kRingBytes + size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
     uint32_t grid = uint32_t(c->cu_count) * uint32_t(per_cu);
     const uint32_t chunk = p->sample_chunk ? p->sample_chunk : 64u;
     const uint32_t n_chunks = (p->samples_per_pixel + chunk - 1) / chunk;
-    const uint64_t work64 = uint64_t(my_tiles) * 64u * n_chunks;
-    if (work64 >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "more than 2^32 (pixel, chunk) work units");
+    const uint32_t unit_chunks = ZRT_UNIT_CHUNKS;
+    const uint32_t n_groups = (n_chunks + unit_chunks - 1) / unit_chunks;
+    const uint64_t work64 = uint64_t(my_tiles) * n_groups;  // units: (tile, group of chunks)
+    if (uint64_t(my_tiles) * 64u * n_chunks >= (1ull << 32))
+      return fail(ZRT_E_UNSUPPORTED, "more than 2^32 (pixel, chunk) work items");
     const uint32_t work = uint32_t(work64);
-    grid = std::max(1u, std::min(grid, (work + zrt::kBlock - 1) / zrt::kBlock));
+    // one wave per unit at the start; more waves than units would only idle
+    grid = std::max(1u, std::min(grid, (work + (zrt::kBlock / 64) - 1) / (zrt::kBlock / 64)));
     const uint64_t n_partial = uint64_t(my_tiles) * 64u * n_chunks;
     if (c->partial.n < n_partial) c->partial.alloc(n_partial);
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
@@ -1324,11 +1379,12 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.stack_depth = stack_depth;
     a.wnodes = c->wnodes.p;
-    a.wleaves = c->wleaves.p;
     a.n_lanes = uint32_t(n_lanes);
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
     a.chunk = chunk;
     a.n_chunks = n_chunks;
+    a.unit_chunks = unit_chunks;
+    a.n_groups = n_groups;
 
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
@@ -1385,7 +1441,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->shade_fetches = h[zrt::kShades];
     out->texel_fetches = h[zrt::kTexels];
     out->leaf_visits = h[zrt::kLeaves];
-    out->node_bytes = c->last_mode == 3 ? 128 : 32;
+    out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
     out->wide_nodes = c->n_wide;
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
@@ -1399,6 +1455,21 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->bvh_max_depth = c->bvh_depth;
     out->n_gpus = 1;
     if (h[zrt::kErrorSlot] != 0) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_debug_counters(zrt_ctx* c, uint64_t* out, uint32_t n) {
+  if (!c || !out) return fail(ZRT_E_INVALID, "null argument");
+  if (!c->launched) return fail(ZRT_E_INVALID, "no kernel launched on this context yet");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long h[zrt::kScratchSlots] = {0};
+    HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n && i < uint32_t(zrt::kScratchSlots); ++i) out[i] = h[i];
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
