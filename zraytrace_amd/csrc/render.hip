@@ -73,7 +73,7 @@ struct KArgs {
   uint32_t width, height, xbound, spp, max_depth;
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
-  uint32_t chunk, n_chunks, unit_chunks, n_groups;
+  uint32_t chunk, n_chunks, unit_chunks, n_groups, sync;
   unsigned long long seed_mix;
 };
 
@@ -101,11 +101,9 @@ constexpr int kBlock = 256;
 #ifndef ZRT_UNIT_CHUNKS
 #define ZRT_UNIT_CHUNKS 1  // chunks of one pixel per work unit (a unit = 8x8 tile x this many chunks)
 #endif
-#ifndef ZRT_UNIT_RING
-#define ZRT_UNIT_RING 4    // units a wave keeps in flight
+#ifndef ZRT_SYNC_SAMPLES
+#define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
 #endif
-constexpr uint32_t kUnitRing = ZRT_UNIT_RING;
-constexpr uint32_t kRingBytes = (kBlock / 64) * kUnitRing * 4;
 
 // ---------------------------------------------------------------------------
 // RNG: std.rand DefaultPrng restated per (pixel, sample)
@@ -607,16 +605,13 @@ template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int
 __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  // LDS: [per-wave unit ring: kWavesPerBlock x kUnitRing u32][traversal stack]
-  uint32_t* ring = reinterpret_cast<uint32_t*>(lds_raw) + (threadIdx.x >> 6) * kUnitRing;
-  StackT* stk = reinterpret_cast<StackT*>(lds_raw + kRingBytes) + threadIdx.x;
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   const int lane = (int)__lane_id();
   const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
 
-  bool need = true, done = false, in_sample = false;
+  bool active = false, in_sample = false;  // active: this lane still has samples in the wave's unit
   uint32_t px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
-  uint32_t seq = 0, chunk_j = 0, chunk_end = 0;  // this lane's place in the wave's unit sequence
-  uint32_t acquired = 0;                          // units the wave has taken (wave-uniform)
+  uint32_t gate = 0, unit_end = 0;  // wave-uniform: lanes run samples < gate; the unit ends at unit_end
   uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -629,44 +624,41 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
   for (;;) {
     uint64_t t0 = prof_stamp();
-    // ---- work: the WAVE takes units (local tile lt, group of unit_chunks
-    // chunks) from the global counter, one atomic per unit; lane p works on
-    // pixel p of the wave's units in sequence.  The 64 lanes of a wave so
-    // stay on one or two 8x8 tiles (coherent camera rays) while each lane
-    // still moves on by itself.  The wave keeps its last kUnitRing units in
-    // LDS and takes a new one only when no lane still works kUnitRing behind.
-    const bool want_new = need && !done && seq == acquired;
-    if (__ballot(want_new) != 0ull && __ballot(!done && seq + kUnitRing <= acquired) == 0ull) {
-      if (lane == 0) ring[acquired % kUnitRing] = atomicAdd(a.work_counter, 1u);
-      ++acquired;
-    }
-    if (need && !done && seq < acquired) {
-      const uint32_t u = ring[seq % kUnitRing];
-      if (u >= a.total_work) {
-        done = true;  // the counter is exhausted; later units are too
+    // ---- work: the WAVE takes units (local tile lt, a group of unit_chunks
+    // chunks) from the global counter, one atomic per unit; lane p renders
+    // pixel p of the unit's 8x8 tile.  The lanes run their paths on their own
+    // but wait for each other every sync samples (gate), so the wave keeps
+    // entering traversal and shading together and its camera rays stay
+    // coherent: divergence, not memory, bounds this loop.
+    const bool runnable = active && sample < gate;
+    if (__ballot(runnable) == 0ull) {
+      if (__ballot(active) != 0ull) {
+        gate = min(gate + a.sync, unit_end);
       } else {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.work_counter, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= a.total_work) break;  // the counter is exhausted
         const uint32_t lt = u / a.n_groups, g = u - lt * a.n_groups;
         const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
         px = (t % a.tiles_x) * 8u + ((uint32_t)lane & 7u);
         py = (t / a.tiles_x) * 8u + ((uint32_t)lane >> 3);
-        if (px < a.xbound && py < a.height) {  // else: finalize writes black
-          need = false;
-          chunk_j = g * a.unit_chunks;
-          chunk_end = min(chunk_j + a.unit_chunks, a.n_chunks);
-          slot = (lt * 64u + (uint32_t)lane) * a.n_chunks + chunk_j;
-          sample = chunk_j * a.chunk;
-          sample_end = min(sample + a.chunk, a.spp);
-          acc_r = acc_g = acc_b = 0.0f;
-          in_sample = false;
-          offset = (uint64_t)py * a.width + px;
-        } else {
-          ++seq;
-        }
+        const uint32_t chunk_j = g * a.unit_chunks;
+        sample = chunk_j * a.chunk;
+        unit_end = min(min(chunk_j + a.unit_chunks, a.n_chunks) * a.chunk, a.spp);
+        gate = min(sample + a.sync, unit_end);
+        active = px < a.xbound && py < a.height;  // else: finalize writes black
+        slot = (lt * 64u + (uint32_t)lane) * a.n_chunks + chunk_j;
+        sample_end = min(sample + a.chunk, a.spp);
+        acc_r = acc_g = acc_b = 0.0f;
+        in_sample = false;
+        offset = (uint64_t)py * a.width + px;
       }
+      if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[0] += t - t0; }
+      continue;
     }
-    if (__ballot(!done) == 0ull) break;
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[0] += t - t0; t0 = t; }
-    if (done || need) continue;
+    if (!runnable) continue;
 
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
     if (!in_sample) {
@@ -825,14 +817,10 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       in_sample = false;
       if (++sample == sample_end) {  // chunk done: its sequential sum
         a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
-        if (++chunk_j < chunk_end) {  // next chunk of this unit
-          ++slot;
-          sample_end = min(sample + a.chunk, a.spp);
-          acc_r = acc_g = acc_b = 0.0f;
-        } else {
-          ++seq;
-          need = true;
-        }
+        ++slot;
+        sample_end = min(sample + a.chunk, a.spp);
+        acc_r = acc_g = acc_b = 0.0f;
+        active = sample < unit_end;
       }
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
@@ -1322,7 +1310,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint32_t stack_depth = mode == 3 ? c->wide_stack : c->stack_depth;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
     const size_t lds =
-        zrt::kRingBytes + size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
+        size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
@@ -1385,6 +1373,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_chunks = n_chunks;
     a.unit_chunks = unit_chunks;
     a.n_groups = n_groups;
+    a.sync = ZRT_SYNC_SAMPLES;
 
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
