@@ -56,7 +56,7 @@ def pmc_traffic(config):
         return None, None
     if d.get("config") != config:
         return None, None
-    return d.get("hbm_bytes_per_launch"), d.get("source")
+    return d.get("hbm_bytes_per_launch"), d
 
 
 def cpu_baseline(scene, seconds_hint):
@@ -171,7 +171,9 @@ def main():
         achieved = algo / avg_kernel_s / 1e9
         pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
-        traffic, traffic_src = pmc_traffic(pmc_key)
+        traffic, pmc = pmc_traffic(pmc_key)
+        traffic_src = pmc.get("source") if pmc else None
+        sq = (pmc or {}).get("sq") or {}
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -206,7 +208,15 @@ def main():
                                      "prim_tests": round(diag["prim_tests"] / max(1, diag["rays_processed"]), 2),
                                      "bytes": round(algo / max(1, diag["rays_processed"]), 1)},
                          "counters_from": "one untimed ZRT_FLAG_STATS launch (kernel "
-                                          f"{diag_kernel_ms:.1f} ms)"},
+                                          f"{diag_kernel_ms:.1f} ms)",
+                         "note": "algorithmic bytes are what each ray's node/primitive/material reads and "
+                                 "path-state writes touch; the scene (~0.5 MB for the bunny) is L1/L2-resident, "
+                                 "so they are served by the caches and frac > 1 against HBM means the loop is not "
+                                 "HBM-bound (traffic = what actually reached HBM). The binding limits are "
+                                 "dependent-load latency and VALU issue (DESIGN.md section 4); see valu_*.",
+                         "valu_lane_util": sq.get("valu_lane_util"),
+                         "valu_insts_per_ray": (round(sq["SQ_INSTS_VALU"] / max(1, st["rays_processed"]), 2)
+                                                if sq.get("SQ_INSTS_VALU") else None)},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
         }
         if world == 1 and not args.no_cpu_baseline:

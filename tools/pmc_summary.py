@@ -5,6 +5,8 @@ Reads <dir>/pmc_fetch/run_counter_collection.csv and <dir>/pmc_write/..., and
 writes per-kernel FETCH_SIZE / WRITE_SIZE plus the corrected HBM bytes per
 launch of the render kernel: (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950
 FETCH_SIZE counts half the bytes of wide streaming reads: MI355X_MICROARCH.md §HBM).
+With a <dir>/pmc_sq pass it also adds the SQ instruction counters per launch and
+the VALU lane utilisation SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU).
 """
 import csv
 import json
@@ -23,6 +25,19 @@ def main():
                 k = res["kernels"].setdefault(r["Kernel_Name"].split("(")[0], {})
                 k[ctr + "_KB"] = float(r["Counter_Value"])
                 k["duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    sq = os.path.join(d, "pmc_sq", "run_counter_collection.csv")
+    if os.path.exists(sq):
+        with open(sq) as f:
+            for r in csv.DictReader(f):
+                if "zrt::" not in r["Kernel_Name"]:
+                    continue
+                k = res["kernels"].setdefault(r["Kernel_Name"].split("(")[0], {})
+                sqd = k.setdefault("sq", {})
+                sqd[r["Counter_Name"]] = sqd.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for k in res["kernels"].values():
+            q = k.get("sq")
+            if q and q.get("SQ_ACTIVE_INST_VALU"):
+                q["valu_lane_util"] = round(q["SQ_THREAD_CYCLES_VALU"] / (64.0 * q["SQ_ACTIVE_INST_VALU"]), 4)
     for name, k in res["kernels"].items():
         if "FETCH_SIZE_KB" in k and "WRITE_SIZE_KB" in k:
             k["hbm_bytes_per_launch_corrected"] = int((2 * k["FETCH_SIZE_KB"] + k["WRITE_SIZE_KB"]) * 1024)

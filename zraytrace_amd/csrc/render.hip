@@ -439,17 +439,12 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const uint32_t cap = a.stack_depth;
   const float inf = __builtin_inff();
   uint32_t sp = 0;
-  int32_t cur = 0;  // the root wide node
+  const float4* q = a.wnodes;  // the root wide node
+  float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], ra = q[6];
   for (;;) {
-    const float4* q = a.wnodes + 8 * cur;
+    int r0 = as_int(ra.x), r1 = as_int(ra.y), r2 = as_int(ra.z), r3 = as_int(ra.w);
     float k0, k1, k2, k3;
-    int r0, r1, r2, r3;
     {
-      const float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], ra = q[6];
-      r0 = as_int(ra.x);
-      r1 = as_int(ra.y);
-      r2 = as_int(ra.z);
-      r3 = as_int(ra.w);
       const float tb = best_t * 1.0000153f;
       k0 = wide_slot(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, tb, r0 < 0);
       k1 = wide_slot(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, tb, r1 < 0);
@@ -460,20 +455,10 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
       ++c_nodes;
       c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
     }
-    if ((r0 < 0 && k0 != inf) || (r1 < 0 && k1 != inf) || (r2 < 0 && k2 != inf) || (r3 < 0 && k3 != inf)) {
-      const float4 rb = q[7];
-#define ZRT_WIDE_LEAF(K, RB)                                                        \
-  if (r##K < 0 && k##K != inf) {                                                    \
-    const int pb = as_int(RB);                                                      \
-    prim_test<true, STATS>(a.prims, r##K, r, best_t, best, c_tri, c_sph);           \
-    if (pb != r##K) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
-  }
-      ZRT_WIDE_LEAF(0, rb.x)
-      ZRT_WIDE_LEAF(1, rb.y)
-      ZRT_WIDE_LEAF(2, rb.z)
-      ZRT_WIDE_LEAF(3, rb.w)
-#undef ZRT_WIDE_LEAF
-    }
+    // leaf slots that pass: their primitive refs (a in r_k, b in the node's last float4)
+    const int l0 = r0 < 0 && k0 != inf ? r0 : 0, l1 = r1 < 0 && k1 != inf ? r1 : 0;
+    const int l2 = r2 < 0 && k2 != inf ? r2 : 0, l3 = r3 < 0 && k3 != inf ? r3 : 0;
+    const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
     k0 = r0 < 0 ? inf : k0;
     k1 = r1 < 0 ? inf : k1;
     k2 = r2 < 0 ? inf : k2;
@@ -484,6 +469,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     cswap(k0, r0, k2, r2);
     cswap(k1, r1, k3, r3);
     cswap(k1, r1, k2, r2);
+    int32_t next = -1;
     if (k0 != inf) {
       // push the farther inner children (farthest first), continue with the nearest
       if (k3 != inf) {
@@ -502,12 +488,30 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
         atomicOr(a.error_flag, 1u);
         sp = cap;
       }
-      cur = r0;
-      continue;
+      next = r0;
+    } else if (sp != 0) {
+      --sp;
+      next = (int32_t)stk[sp * stride];
     }
-    if (sp == 0) return;
-    --sp;
-    cur = (int32_t)stk[sp * stride];
+    if ((l0 | l1 | l2 | l3) != 0) {
+      const float4 rb = leaf_q[7];
+#define ZRT_WIDE_LEAF(L, RB)                                                        \
+  if (L != 0) {                                                                     \
+    const int pb = as_int(RB);                                                      \
+    prim_test<true, STATS>(a.prims, L, r, best_t, best, c_tri, c_sph);              \
+    if (pb != L) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
+  }
+      ZRT_WIDE_LEAF(l0, rb.x)
+      ZRT_WIDE_LEAF(l1, rb.y)
+      ZRT_WIDE_LEAF(l2, rb.z)
+      ZRT_WIDE_LEAF(l3, rb.w)
+#undef ZRT_WIDE_LEAF
+    }
+    if (next < 0) return;
+    // (issuing these loads before the leaves above was measured slower: the
+    // 28 extra live registers spill)
+    q = a.wnodes + 8 * next;
+    mnx = q[0]; mny = q[1]; mnz = q[2]; mxx = q[3]; mxy = q[4]; mxz = q[5]; ra = q[6];
   }
 }
 
