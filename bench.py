@@ -25,6 +25,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "Mrays/s + achieved HBM GB/s, bunny BVH @ 2048², 1024spp, 1/2/4/8 GPUs"
+SCENES = {0: "manAndBall: models/Man_LOD3.obj + ground sphere", 1: "threeBalls: 7 spheres",
+          2: "bunnyAndBall: models/bunny.obj + ground sphere", 3: "teapotAndBall: models/teapot.obj + ground sphere",
+          4: "teapotAndBallCircle: teapot + ring of spheres"}  # scenes.zig:267-277
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -186,8 +189,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: the reference's own scene 2 (models/bunny.obj + ground sphere), no dataset",
-            "config": {"workload": f"scene {args.scene} (bunnyAndBall) BVH, {args.width}x{args.height} @ "
+            "data": f"synthetic: the reference's own scene {args.scene} ({SCENES[args.scene]}), no dataset",
+            "config": {"workload": f"scene {args.scene} ({SCENES[args.scene].split(':')[0]}) "
+                                   f"{'BVH' if st['used_bvh'] else 'list'}, {args.width}x{args.height} @ "
                                    f"{args.spp} spp, max depth {args.depth}",
                        "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                        "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk,
@@ -217,6 +221,8 @@ def main():
                          "valu_lane_util": sq.get("valu_lane_util"),
                          "valu_insts_per_ray": (round(sq["SQ_INSTS_VALU"] / max(1, st["rays_processed"]), 2)
                                                 if sq.get("SQ_INSTS_VALU") else None)},
+            "accel": {"reference_bvh_nodes": diag["bvh_nodes"], "reference_bvh_depth": diag["bvh_max_depth"],
+                      "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
         }
         if world == 1 and not args.no_cpu_baseline:
