@@ -62,21 +62,21 @@ def pmc_traffic(config):
     return d.get("hbm_bytes_per_launch"), d
 
 
-def cpu_baseline(scene, seconds_hint):
+def cpu_baseline(scene, scene_index, depth):
     """The oracle (single-threaded C restatement, reference RNG stream) on a
-    bounded sample of the same scene: 128x128 @ 4 spp, depth 20."""
+    bounded sample of the same scene: 128x128 @ 4 spp at the bench's depth."""
     import zraytrace_amd as z
     from oracle import oracle_py as O
     w = h = 128
     spp = 4
-    p = z.RenderParams(w, h, spp, 20, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
+    p = z.RenderParams(w, h, spp, depth, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
     t0 = time.perf_counter()
     _, st = O.render(scene.view, scene.camera, p)
     dt = time.perf_counter() - t0
     return {"value": st["rays_processed"] / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/ (C restatement of the Zig path, reference RNG stream), scene 2 bunny, "
-                      f"{w}x{h} @ {spp} spp, depth 20: {st['rays_processed']} rays in {dt:.1f} s on 1 core "
-                      f"({os.cpu_count()} visible)"}
+            "sample": f"oracle/ (C restatement of the Zig path, reference RNG stream), scene {scene_index} "
+                      f"({SCENES[scene_index].split(':')[0]}), {w}x{h} @ {spp} spp, depth {depth}: "
+                      f"{st['rays_processed']} rays in {dt:.1f} s on 1 core ({os.cpu_count()} visible)"}
 
 
 def main():
@@ -227,7 +227,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[rank 0] cpu baseline (oracle, 1 core) ...")
-            out["cpu_baseline"] = cpu_baseline(scene, 10)
+            out["cpu_baseline"] = cpu_baseline(scene, args.scene, args.depth)
         print(json.dumps(out), flush=True)
 
     ctx.close()
