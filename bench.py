@@ -16,6 +16,7 @@ Run: python bench.py [--gpus N --steps K --warmup W]
      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -92,6 +93,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--traversal", choices=["fast", "reference", "binary"], default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK)")
     args = ap.parse_args()
 
     import torch
@@ -102,9 +106,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.device is not None:
+        local = args.device
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import zraytrace_amd as z
     scene = z.load_scene(args.scene)
@@ -156,9 +165,10 @@ def main():
     diag = ctx.stats()
     diag_kernel_ms = ctx.kernel_ms()
     assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
+    red = "cuda" if args.dist_backend == "nccl" else "cpu"
     rays = torch.tensor([float(st["rays_processed"]), float(st["samples_processed"])], dtype=torch.float64,
-                        device="cuda")
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+                        device=red)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=red)
     if world > 1:
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -166,6 +176,8 @@ def main():
     elapsed = el.item()
 
     if rank == 0:
+        # hash of the last timed step's assembled frame: identical for every N
+        frame_sha1 = hashlib.sha1(frame.cpu().numpy().tobytes()).hexdigest()
         value = total_rays * args.steps / elapsed / 1e6
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
         chunk = args.chunk or 64
@@ -224,6 +236,7 @@ def main():
             "accel": {"reference_bvh_nodes": diag["bvh_nodes"], "reference_bvh_depth": diag["bvh_max_depth"],
                       "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
+            "frame_sha1": frame_sha1,
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[rank 0] cpu baseline (oracle, 1 core) ...")

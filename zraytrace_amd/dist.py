@@ -33,8 +33,11 @@ def gather_tiles(tiles, counts, rank, world, dst=0, group=None):
     import torch.distributed as dist
     if world == 1:
         return tiles[: counts[0] * 64 * 3]
-    bufs = [torch.empty_like(tiles) for _ in range(world)] if rank == dst else None
-    dist.gather(tiles, bufs, dst=dst, group=group)
+    send = tiles
+    if tiles.is_cuda and dist.get_backend(group) == "gloo":
+        send = tiles.cpu()  # gloo gathers host tensors (multi-rank rehearsal on one GPU)
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    return torch.cat([b[: c * 64 * 3] for b, c in zip(bufs, counts)])
+    return torch.cat([b[: c * 64 * 3] for b, c in zip(bufs, counts)]).to(tiles.device)
