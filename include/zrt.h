@@ -262,9 +262,12 @@ int zrt_ctx_last_kernel_ms(zrt_ctx* ctx, double* ms);
 typedef struct zrt_scene_data zrt_scene_data;
 
 /* Build scene `scene_index` as scenes.zig:267-277 does (0 man+ball, 1 seven
- * spheres, 2 bunny+ball, 3 teapot+ball, 4 teapot+ball circle, 5 goat).  The
- * camera is returned in *camera; the scene view stays valid until
- * zrt_scene_free.  Unknown index -> ZRT_E_INVALID (SceneError.UnkownSceneIndex). */
+ * spheres, 2 bunny+ball, 3 teapot+ball, 4 teapot+ball circle, 5 goat - needs
+ * high_poly_goat.obj, which the reference does not ship: ZRT_E_IO without it),
+ * plus 6: the textured, subdivided teapot that stands in for config C5
+ * (DESIGN.md section 4).  The camera is returned in *camera; the scene view
+ * stays valid until zrt_scene_free.  Unknown index -> ZRT_E_INVALID
+ * (SceneError.UnkownSceneIndex). */
 int zrt_scene_load(uint32_t scene_index, const char* assets_dir,
                    zrt_scene_data** out, zrt_camera* camera);
 const zrt_scene* zrt_scene_view(const zrt_scene_data* data);

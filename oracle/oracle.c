@@ -9,6 +9,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "zig_std.h"
 
@@ -598,6 +599,12 @@ static int validate(const zrt_scene* scene, const zrt_camera* camera, const zrt_
   return ZRT_OK;
 }
 
+static double now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 static uint64_t counter_key(uint64_t pixel, uint32_t sample, uint64_t seed) {
   return ((pixel << 16) | (uint64_t)sample) + seed * 0x9E3779B97F4A7C15ULL;
 }
@@ -608,9 +615,11 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
   if (rc) return rc;
   if (y1 > p->height || y0 > y1) return ZRT_E_INVALID;
   if (p->rng_mode == ZRT_RNG_REFERENCE_STREAM && y0 != 0) return ZRT_E_INVALID;
+  const double t_start = now_ms();
   Scene sc;
   rc = scene_build(&sc, scene, p->bounded_volume_hierarchy != 0);
   if (rc) { scene_free(&sc); return rc; }
+  const double t_built = now_ms();  /* raytrace.zig:150: preprocess timed apart from rendering */
 
   zs_rng global;
   zs_rng_init(&global, (int)p->prng, p->seed);
@@ -673,6 +682,8 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
     stats->bvh_nodes = sc.bvh.n;
     stats->bvh_max_depth = (uint32_t)sc.bvh.max_depth;
     stats->n_gpus = 0;
+    stats->preprocess_ms = t_built - t_start;
+    stats->render_ms = now_ms() - t_built;
   }
   scene_free(&sc);
   return ZRT_OK;

@@ -23,9 +23,9 @@ def _ensure_built():
     lib = os.path.join(REPO, "zraytrace_amd", "libzrt.so")
     if not os.path.exists(lib):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "zraytrace_amd", "csrc")], check=True)
-    orc = os.path.join(REPO, "oracle", "liboracle.so")
-    if not os.path.exists(orc):
-        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    # the oracle is rebuilt whenever it is older than its sources or include/zrt.h
+    # (a stale build would read zrt_stats with an old layout); a second of gcc
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
 
 
 _ensure_built()

@@ -104,6 +104,23 @@ def test_render_bit_exact_vs_oracle(scenes, case, traversal):
         assert gs["node_visits"] == rs["node_visits"]
 
 
+def test_c5_substitute_bit_exact(scenes):
+    """Scene 6, the stated C5 substitute: 1.6 M subdivided teapot triangles
+    (reference BVH 1 894 803 nodes, depth 39) with image-textured lambertians on both surfaces, so the
+    scene and textures exceed L2.  FAST and REFERENCE traversal against the
+    oracle (whose reference-order traversal of this tree bounds the size)."""
+    s = scenes(6)
+    p = z.RenderParams(16, 16, 1, 4)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert rs["used_bvh"] and rs["bvh_nodes"] == 1_894_803
+    for trav in (z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE):
+        p.traversal = trav
+        gpu, gs = z.render(s, s.camera, p)
+        assert_bit_exact(gpu, ref)
+        for k in COUNTERS:
+            assert gs[k] == rs[k], k
+
+
 def test_nonsquare_and_ragged_tiles(scenes):
     """height < width: raytrace.zig:168 leaves columns x >= height black; 8x8
     tiles overhang both edges (37 x 21)."""

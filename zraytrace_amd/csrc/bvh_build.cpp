@@ -11,8 +11,13 @@
 //       last trial left (bvh.zig:85-120).
 //   pseudoSA(box) = 2 * (dx^2 + dy^2 + dz^2)                (aabb.zig:99-105)
 //   node box = initAabb(left, right)                        (bvh.zig:164)
-// std.sort.sort is a stable sort, so std::stable_sort with the same strict
-// comparator yields the identical permutation.
+// std.sort.sort is a stable sort, so any stable sort with the same strict
+// comparator yields the identical permutation.  Two consequences used here:
+// re-sorting a slice on the axis it is already sorted on changes nothing, so
+// each axis is sorted once (not once per split trial); and a stable LSD radix
+// sort on order-preserving u32 images of the keys (-0 mapped to +0, which the
+// comparator treats as equal) is the same permutation in O(n).  NaN keys (no
+// strict weak order) fall back to std::stable_sort.
 //
 // Unlike the reference (one heap Surface per node, pointer chasing), nodes are
 // emitted into a flat array in depth-first pre-order (left first), and the
@@ -101,10 +106,44 @@ struct Builder {
     return box_min_max(mn, mx);
   }
 
+  std::vector<uint32_t> key_a, key_b, idx_b;  // radix sort scratch
+
   void sort_axis(int axis, size_t lo, size_t hi) {
     const std::vector<Box>& pb = pbox;
-    std::stable_sort(order.begin() + lo, order.begin() + hi,
-                     [&pb, axis](uint32_t a, uint32_t b) { return pb[a].mid[axis] < pb[b].mid[axis]; });
+    const size_t n = hi - lo;
+    bool has_nan = false;
+    for (size_t i = lo; i < hi && !has_nan; ++i) has_nan = std::isnan(pb[order[i]].mid[axis]);
+    if (n < 64 || has_nan) {
+      std::stable_sort(order.begin() + lo, order.begin() + hi,
+                       [&pb, axis](uint32_t a, uint32_t b) { return pb[a].mid[axis] < pb[b].mid[axis]; });
+      return;
+    }
+    key_a.resize(n);
+    key_b.resize(n);
+    idx_b.resize(n);
+    uint32_t* idx_a = order.data() + lo;
+    for (size_t i = 0; i < n; ++i) {
+      const float f = pb[idx_a[i]].mid[axis];
+      uint32_t u;
+      std::memcpy(&u, &f, 4);
+      if (f == 0.0f) u = 0;  // -0 == +0 under `<`
+      key_a[i] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    }
+    uint32_t *ka = key_a.data(), *kb = key_b.data(), *ia = idx_a, *ib = idx_b.data();
+    for (int shift = 0; shift < 32; shift += 8) {
+      size_t count[257] = {0};
+      for (size_t i = 0; i < n; ++i) ++count[((ka[i] >> shift) & 0xffu) + 1];
+      if (count[((ka[0] >> shift) & 0xffu) + 1] == n) continue;  // one digit value: pass is the identity
+      for (int d = 0; d < 256; ++d) count[d + 1] += count[d];
+      for (size_t i = 0; i < n; ++i) {
+        const size_t at = count[(ka[i] >> shift) & 0xffu]++;
+        kb[at] = ka[i];
+        ib[at] = ia[i];
+      }
+      std::swap(ka, kb);
+      std::swap(ia, ib);
+    }
+    if (ia != idx_a) std::memcpy(idx_a, ia, n * sizeof(uint32_t));
   }
 
   // bvh.zig:85-120
@@ -123,9 +162,9 @@ struct Builder {
       n_splits = 3;
     }
     for (int axis = 0; axis < 3; ++axis) {
+      sort_axis(axis, lo, hi);  // (the reference sorts before every split; repeats are no-ops)
       for (int k = 0; k < n_splits; ++k) {
         const size_t split = splits[k];
-        sort_axis(axis, lo, hi);
         const float area = pseudo_area(range_box(lo + split, hi)) + pseudo_area(range_box(lo, lo + split));
         const float ratio = area / total_area;
         if (ratio < best_ratio) {
@@ -135,7 +174,7 @@ struct Builder {
         }
       }
     }
-    sort_axis(best_axis, lo, hi);
+    if (best_axis != 2) sort_axis(best_axis, lo, hi);  // from the z-sorted order, as the reference
     return best_split;
   }
 
