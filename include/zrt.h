@@ -278,6 +278,15 @@ void zrt_scene_free(zrt_scene_data* data);
 int zrt_obj_read(const char* path, uint32_t material, zrt_prim** out_prims, uint32_t* n_prims);
 void zrt_free(void* p);
 
+/* ---- image output (the caller side: main.zig:33 writes the rendered image) -- *
+ * `rgb` is a framebuffer as zrt_render returns it (row 0 = bottom).
+ * PNG: png_image.zig:96-148 - 8-bit RGB, top row first,
+ *      u8(std.math.clamp(255.999 * c, 0, 255)) per channel.
+ * PPM: ppm_image.zig - plain P3 text, u32(c * 255.999) clamped to [0, 255].
+ * Unopenable path -> ZRT_E_IO (PngError.FailedToOpenFile). */
+int zrt_image_write_png(const char* path, const float* rgb, uint32_t width, uint32_t height);
+int zrt_image_write_ppm(const char* path, const float* rgb, uint32_t width, uint32_t height);
+
 /* ---- BVH export (parity of bvh.zig:62-185 against the oracle) ------------- *
  * Node i: box min/max and two children.  A child c >= 0 is a node index; a
  * child c < 0 is primitive (-c - 1) in reference list order.  Leaves are

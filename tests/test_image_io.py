@@ -1,0 +1,118 @@
+"""The caller-side image writers (png_image.zig:96-148, ppm_image.zig) and the
+command line (main.zig) over the C ABI.  CPU-only except the marked test."""
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import zraytrace_amd as z
+from zraytrace_amd import _ffi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(REPO, "zraytrace_amd", "zrt-raytrace")
+
+
+def png_quantize(img):
+    """u8(std.math.clamp(255.999 * c, 0, 255)) in f32, math.min/max as `x < y ? x : y`."""
+    v = (np.float32(255.999) * img.astype(np.float32)).astype(np.float32)
+    m = np.where(v < 255, v, np.float32(255))        # min(v, 255): NaN -> 255
+    c = np.where(np.float32(0) > m, np.float32(0), m)  # max(0, m)
+    return np.trunc(c).astype(np.uint8)[::-1]         # top row first
+
+
+def ppm_quantize(img):
+    x = (img.astype(np.float32) * np.float32(255.999)).astype(np.float32)
+    out = np.where(x >= 0, np.minimum(np.trunc(np.nan_to_num(x, nan=0.0, posinf=255.0)), 255), 0)
+    return out.astype(np.uint32)[::-1]
+
+
+def decode_png(path):
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, ihdr = 8, b"", None
+    while pos < len(data):
+        n, typ = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(typ + body) & 0xffffffff
+        if typ == b"IHDR":
+            ihdr = struct.unpack(">IIBBBBB", body)
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    w, h, bits, color, _, _, interlace = ihdr
+    assert (bits, color, interlace) == (8, 2, 0)
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 3 * w)
+    assert (raw[:, 0] == 0).all()  # filter type None on every row
+    return raw[:, 1:].reshape(h, w, 3)
+
+
+def test_png_matches_reference_quantization(tmp_path):
+    rng = np.random.default_rng(3)
+    img = rng.uniform(-0.2, 1.2, (13, 17, 3)).astype(np.float32)
+    img[0, 0] = [np.nan, -0.0, 1.0]
+    img[0, 1] = [np.inf, -np.inf, 0.999]
+    img[1, 0] = [1.0 / 255.999, 0.5, 254.5 / 255.999]
+    p = str(tmp_path / "out.png")
+    z.write_png(p, img)
+    np.testing.assert_array_equal(decode_png(p), png_quantize(img))
+
+
+def test_ppm_matches_reference_format(tmp_path):
+    rng = np.random.default_rng(4)
+    img = rng.uniform(0.0, 1.0, (5, 7, 3)).astype(np.float32)
+    p = str(tmp_path / "out.ppm")
+    z.write_ppm(p, img)
+    text = open(p).read()
+    head = f"P3\n# filename: {p}\n# The P3 = colors are in ASCII\n# Image width and height\n7 5\n" \
+           "# Max color value\n255\n# RGB triplets\n"
+    assert text.startswith(head)
+    rows = text[len(head):].split("\n")[:-1]
+    want = ppm_quantize(img)
+    for y, row in enumerate(rows):
+        assert row == "".join(f"{r:>3} {g:>3} {b:>3}  " for r, g, b in want[y])
+
+
+def test_writer_errors(tmp_path):
+    img = np.zeros((2, 2, 3), np.float32)
+    with pytest.raises(z.ZrtError) as e:
+        z.write_png(str(tmp_path / "no" / "such" / "dir.png"), img)
+    assert e.value.code == _ffi.ZRT_E_IO
+
+
+def test_cli_arguments_and_no_device():
+    r = subprocess.run([CLI, "32", "70000", "4", "5", "1", "x.png"], capture_output=True, text=True)
+    assert r.returncode == 1
+    assert r.stderr.startswith("raytrace\nUSAGE;\nraytrace width heigth samples depth scene_index filename\n")
+    assert "error: Overflow" in r.stderr
+    r = subprocess.run([CLI, "32", "32"], capture_output=True, text=True)
+    assert r.returncode == 1 and "error: missing argument" in r.stderr
+    import torch
+    if not torch.cuda.is_available():  # the HIP path fails loudly, no CPU fallback
+        r = subprocess.run([CLI, "8", "8", "1", "2", "1", "x.png"], capture_output=True, text=True)
+        assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_renders_oracle_image(tmp_path, scenes):
+    """main.zig end to end: the CLI's PNG is the oracle image through
+    png_image.zig's quantization, and its summary lines carry the counters."""
+    from oracle import oracle_py as O
+    out = str(tmp_path / "scene1.png")
+    r = subprocess.run([CLI, "40", "40", "4", "12", "1", out], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    s = scenes(1)
+    ref, rs = O.render(s.view, s.camera, z.RenderParams(40, 40, 4, 12))
+    np.testing.assert_array_equal(decode_png(out), png_quantize(ref))
+    summary = {}
+    for line in r.stderr.splitlines():
+        if line.startswith("  Total ") and line.count(":") == 1:
+            label, value = line.split(":")
+            summary[label.strip()] = value.strip()
+    for label, key in (("Total rays", "rays_processed"), ("Total samples", "samples_processed"),
+                       ("Total background hits", "background_hits"), ("Total pixels", "pixels_processed"),
+                       ("Total reflections", "reflections")):
+        assert int(summary[label]) == rs[key], label

@@ -206,3 +206,17 @@ def debug_rng(prng: int, key: int, n: int, device: int = 0):
     out = np.empty(n, dtype=np.uint64)
     check(lib().zrt_debug_rng(prng, key, out.ctypes.data_as(C.POINTER(C.c_uint64)), n, device))
     return out
+
+
+def write_png(path: str, image) -> None:
+    """png_image.writeFile (png_image.zig:96-148) for a framebuffer[H, W, 3] (row 0 = bottom)."""
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    h, w, _ = img.shape
+    check(lib().zrt_image_write_png(os.fsencode(path), img.ctypes.data_as(C.POINTER(C.c_float)), w, h))
+
+
+def write_ppm(path: str, image) -> None:
+    """ppm_image.writeFile (plain P3) for a framebuffer[H, W, 3] (row 0 = bottom)."""
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    h, w, _ = img.shape
+    check(lib().zrt_image_write_ppm(os.fsencode(path), img.ctypes.data_as(C.POINTER(C.c_float)), w, h))

@@ -124,6 +124,8 @@ SIGNATURES = [
     ("zrt_obj_read", C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.POINTER(Prim)),
                                C.POINTER(C.c_uint32)]),
     ("zrt_free", None, [_P]),
+    ("zrt_image_write_png", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
+    ("zrt_image_write_ppm", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
     ("zrt_bvh_build", C.c_int, [C.POINTER(Scene), C.POINTER(C.POINTER(BvhNode)),
                                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     ("zrt_debug_math", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float),
