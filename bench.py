@@ -42,12 +42,12 @@ def algorithmic_bytes(st, n_work_units, n_pixels):
     """Bytes the sampling loop must touch per launch:
     per node record read (32 B binary/reference node; 128 B wide node, which
     also carries its leaf children's boxes), 48 B per triangle test, 16 B per sphere test,
-    64 B per shaded hit (16 B shade record + 48 B material), 12 B per texel,
+    64 B per shaded hit (16 B shade record + 48 B material), 4 B (8-bit store) or 12 B (f32) per texel,
     32 B per scatter (attenuation pushed + read back), 16 B per chunk sum
     written and read, 12 B per output pixel."""
     tri = st["prim_tests"] - st["sphere_tests"]
     return (st["node_bytes"] * st["node_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
-            + 12 * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
+            + (st["texel_bytes"] or 12) * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 
 def pmc_traffic(config):

@@ -191,6 +191,9 @@ typedef struct zrt_stats {
   uint32_t n_gpus;
   uint32_t node_bytes;    /* bytes of one node record of the traversal used (32 or 128) */
   uint32_t wide_nodes;    /* FAST traversal: 4-wide nodes over the reference leaves */
+  uint32_t texel_bytes;   /* bytes per texel on the device: 4 when every image is exact 8-bit
+                             (c == k/255, png_image.zig:76-89), else 12 (f32 RGB); 0: no images */
+  uint32_t reserved_stats;
 } zrt_stats;
 
 /* ---- entry points -------------------------------------------------------- */

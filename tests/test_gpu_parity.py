@@ -231,3 +231,51 @@ def test_sample_chunks(scenes, chunk):
     ref, rs = O.render(s.view, s.camera, p)
     assert_bit_exact(gpu, ref)
     assert gs["samples_processed"] == rs["samples_processed"] == 16 * 16 * 100
+
+
+def _texture_scene(rng):
+    """Two image-textured spheres over a ground sphere: one image exact 8-bit
+    (stored as RGBX8 on the device), one with arbitrary f32 values (kept f32)."""
+    from zraytrace_amd import _ffi
+    import ctypes as C
+    img8 = (rng.integers(0, 256, (37, 53, 3)).astype(np.float32) / np.float32(255.0)).astype(np.float32)
+    imgf = rng.random((29, 41, 3), dtype=np.float32)
+    imgs = (_ffi.Image * 2)(_ffi.Image(53, 37, img8.ctypes.data_as(C.POINTER(C.c_float))),
+                            _ffi.Image(41, 29, imgf.ctypes.data_as(C.POINTER(C.c_float))))
+    texs = (_ffi.Texture * 3)(_ffi.Texture(_ffi.ZRT_TEX_IMAGE, 0, _ffi.Vec3(0, 0, 0), 0.25, 0.1),
+                              _ffi.Texture(_ffi.ZRT_TEX_IMAGE, 1, _ffi.Vec3(0, 0, 0), 0.0, 0.0),
+                              _ffi.Texture(_ffi.ZRT_TEX_COLOR, 0, _ffi.Vec3(0.4, 0.7, 0.3), 0.0, 0.0))
+    mats = (_ffi.Material * 3)(_ffi.Material(_ffi.ZRT_MAT_LAMBERTIAN, 0, 0.0),
+                               _ffi.Material(_ffi.ZRT_MAT_METAL, 1, 0.0),
+                               _ffi.Material(_ffi.ZRT_MAT_LAMBERTIAN, 2, 0.0))
+    prims = (_ffi.Prim * 3)()
+    for i, (c, r, m) in enumerate((((1.0, -101.5, 4.0), 100.0, 2), ((-1.2, 0.0, 4.0), 1.0, 0),
+                                   ((1.3, 0.0, 4.5), 1.1, 1))):
+        prims[i].kind = _ffi.ZRT_PRIM_SPHERE
+        prims[i].material = m
+        prims[i].center = _ffi.Vec3(*c)
+        prims[i].radius = r
+    scene = _ffi.Scene(prims, 3, 3, mats, texs, 3, 2, imgs)
+    scene._keep = (prims, mats, texs, imgs, img8, imgf)
+    return scene
+
+
+def test_texel_stores_bit_exact():
+    """8-bit-exact images take the RGBX8 + table path, others stay f32; both
+    must give the oracle's image (texture.zig:20-74 on f32 values)."""
+    import ctypes as C
+    s = _texture_scene(np.random.default_rng(11))
+    cam = z.camera_init((0, 0, -3), (0, 0, 4), (0, 1, 0), 45.0, 1.0)
+    p = z.RenderParams(32, 32, 4, 8)
+    gpu, gs = z.render(C.pointer(s), cam, p)
+    ref, rs = O.render(C.pointer(s), cam, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+    assert gs["texel_bytes"] == 12  # one f32 image in the scene
+
+
+def test_eight_bit_texels_selected(scenes):
+    p = z.RenderParams(8, 8, 1, 2)
+    _, gs = z.render(scenes(4), scenes(4).camera, p)
+    assert gs["texel_bytes"] == 4  # earthmap from png_image.zig's byte / 255

@@ -89,7 +89,8 @@ class Stats(C.Structure):
                 ("render_ms", C.c_double), ("gather_ms", C.c_double),
                 ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),
                 ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32),
-                ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32)]
+                ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32),
+                ("texel_bytes", C.c_uint32), ("reserved_stats", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -53,7 +53,8 @@ struct alignas(16) DevMaterial {
   float r, g, b, ior;          // texture color / index of refraction
   float u_off, v_off;          // image texture offsets
   uint32_t kind, tex_kind;     // ZRT_MAT_*, ZRT_TEX_*
-  uint32_t img_w, img_h, img_off, pad;  // image texture (img_off in texels)
+  uint32_t img_w, img_h, img_off;  // image texture (img_off in texels of its store)
+  uint32_t img_u8;                 // 1: the image is stored as 8-bit RGBX (exact k/255), 0: f32 RGB
 };
 
 struct KArgs {
@@ -62,7 +63,9 @@ struct KArgs {
   const float4* __restrict__ shade;
   const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (8 float4 each)
   const DevMaterial* __restrict__ mats;
-  const float* __restrict__ texels;
+  const float* __restrict__ texels;    // f32 RGB images
+  const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
+  const float* __restrict__ lut255;      // k / 255.0f for k = 0..255 (png_image.zig:88)
   float4* __restrict__ att;            // [max_depth][n_lanes]
   float4* __restrict__ partial;        // [tile slot][chunk] chunk sums
   uint32_t* __restrict__ work_counter;
@@ -544,14 +547,14 @@ __device__ __forceinline__ MatReg load_material(const DevMaterial* __restrict__ 
 }
 
 // texture.zig:20-74
-__device__ __forceinline__ V3 albedo(const MatReg& mr, const float* __restrict__ texels, float u, float v) {
+__device__ __forceinline__ V3 albedo(const MatReg& mr, const KArgs& a, float u, float v) {
   if (mr.tex_kind() == ZRT_TEX_COLOR) {
     const float4 c = mr.q[0];
     return mk(c.x, c.y, c.z);
   }
   const float4 m2 = mr.q[2];
-  struct { float u_off, v_off; uint32_t img_w, img_h, img_off; } m = {
-      mr.m1.x, mr.m1.y, __float_as_uint(m2.x), __float_as_uint(m2.y), __float_as_uint(m2.z)};
+  struct { float u_off, v_off; uint32_t img_w, img_h, img_off, img_u8; } m = {
+      mr.m1.x, mr.m1.y, __float_as_uint(m2.x), __float_as_uint(m2.y), __float_as_uint(m2.z), __float_as_uint(m2.w)};
   const float uu_first = 1.0f - u + m.u_off;
   float uu = uu_first;
   if (uu_first > 1.0f) uu = uu_first - 1.0f;
@@ -562,7 +565,12 @@ __device__ __forceinline__ V3 albedo(const MatReg& mr, const float* __restrict__
   else if (uu_first < 0.0f) vv = vv_first + 1.0f;  // texture.zig:66 tests uu_first
   const uint32_t x = texel_index(uu * (float)m.img_w, m.img_w);
   const uint32_t y = texel_index(vv * (float)m.img_h, m.img_h);
-  const float* p = texels + 3ull * ((uint64_t)m.img_off + (uint64_t)y * m.img_w + x);
+  const uint64_t t = (uint64_t)m.img_off + (uint64_t)y * m.img_w + x;
+  if (m.img_u8) {  // 4 B instead of 12 B per texel; the table holds the reference's f32 values
+    const uint32_t px = a.texels8[t];
+    return mk(a.lut255[px & 0xffu], a.lut255[(px >> 8) & 0xffu], a.lut255[(px >> 16) & 0xffu]);
+  }
+  const float* p = a.texels + 3ull * t;
   return mk(p[0], p[1], p[2]);
 }
 
@@ -772,10 +780,10 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
           V3 hv = mk(cs * rr, sn * rr, r1);
           if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
           nd = unit(add(normal, hv));
-          att = albedo(mat, a.texels, tu, tv);
+          att = albedo(mat, a, tu, tv);
         } else if (mkind == ZRT_MAT_METAL) {
           nd = unit(reflect(unit(d), normal));
-          if (dot(nd, normal) > 0.0f) att = albedo(mat, a.texels, tu, tv);
+          if (dot(nd, normal) > 0.0f) att = albedo(mat, a, tu, tv);
           else absorbed = true;
         } else {
           const float ratio = front ? (1.0f / mat.ior()) : mat.ior();
@@ -1054,7 +1062,9 @@ struct zrt_ctx {
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
-  zrt::DevBuf<float> texels;
+  zrt::DevBuf<float> texels, lut255;
+  zrt::DevBuf<uint32_t> texels8;
+  uint32_t texel_bytes = 0;
   zrt::DevBuf<float4> att;
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
   zrt::DevBuf<float4> partial;
@@ -1160,15 +1170,31 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     }
     std::memcpy(&sh.w, &tag, 4);
   }
-  // materials + textures
+  // materials + textures.  An image whose every value is exactly k/255 (what
+  // png_image.zig:76-89 produces) is stored as 8-bit RGBX and expanded through
+  // a table of the same f32 values; any other image stays f32 RGB.
+  float lut[256];
+  for (int k = 0; k < 256; ++k) lut[k] = float(k) / 255.0f;
   std::vector<DevMaterial> mats(s->n_materials);
   std::vector<uint64_t> img_off(s->n_images);
-  uint64_t texel_count = 0;
+  std::vector<uint32_t> img_u8(s->n_images, 0);
+  uint64_t texel_count = 0, texel8_count = 0;
   for (uint32_t i = 0; i < s->n_images; ++i) {
-    img_off[i] = texel_count;
-    texel_count += uint64_t(s->images[i].width) * s->images[i].height;
+    const zrt_image& im = s->images[i];
+    const size_t nv = 3 * size_t(im.width) * im.height;
+    bool exact = true;
+    for (size_t j = 0; j < nv && exact; ++j) {
+      const float v = im.pixels[j];
+      const long k = std::lrint(double(v) * 255.0);
+      exact = k >= 0 && k <= 255 && std::memcmp(&lut[k], &v, 4) == 0;
+    }
+    img_u8[i] = exact ? 1u : 0u;
+    uint64_t& count = exact ? texel8_count : texel_count;
+    img_off[i] = count;
+    count += uint64_t(im.width) * im.height;
   }
-  if (texel_count >= (1ull << 32)) throw Error(ZRT_E_UNSUPPORTED, "more than 2^32 texels");
+  if (texel_count >= (1ull << 32) || texel8_count >= (1ull << 32))
+    throw Error(ZRT_E_UNSUPPORTED, "more than 2^32 texels");
   for (uint32_t i = 0; i < s->n_materials; ++i) {
     const zrt_material& m = s->materials[i];
     DevMaterial dm{};
@@ -1187,20 +1213,36 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
         dm.img_w = s->images[t.image].width;
         dm.img_h = s->images[t.image].height;
         dm.img_off = uint32_t(img_off[t.image]);
+        dm.img_u8 = img_u8[t.image];
       }
     }
     mats[i] = dm;
   }
   std::vector<float> tex(3 * texel_count);
-  for (uint32_t i = 0; i < s->n_images; ++i)
-    std::memcpy(&tex[3 * img_off[i]], s->images[i].pixels,
-                sizeof(float) * 3 * size_t(s->images[i].width) * s->images[i].height);
+  std::vector<uint32_t> tex8(texel8_count);
+  for (uint32_t i = 0; i < s->n_images; ++i) {
+    const zrt_image& im = s->images[i];
+    const size_t np = size_t(im.width) * im.height;
+    if (img_u8[i]) {
+      for (size_t j = 0; j < np; ++j) {
+        uint32_t px = 0;
+        for (int ch = 0; ch < 3; ++ch)
+          px |= uint32_t(std::lrint(double(im.pixels[3 * j + ch]) * 255.0)) << (8 * ch);
+        tex8[img_off[i] + j] = px;
+      }
+    } else {
+      std::memcpy(&tex[3 * img_off[i]], im.pixels, sizeof(float) * 3 * np);
+    }
+  }
+  c->texel_bytes = s->n_images == 0 ? 0u : texel_count == 0 ? 4u : 12u;
   const double t1 = now_ms();
   c->nodes.upload(nodes);
   c->prims.upload(prims);
   c->shade.upload(shade);
   c->mats.upload(mats);
   c->texels.upload(tex);
+  c->texels8.upload(tex8);
+  c->lut255.upload(std::vector<float>(lut, lut + 256));
   c->preprocess_ms = t1 - t0;
   c->upload_ms = now_ms() - t1;
   c->use_bvh = use_bvh;
@@ -1344,6 +1386,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.shade = c->shade.p;
     a.mats = c->mats.p;
     a.texels = c->texels.p;
+    a.texels8 = c->texels8.p;
+    a.lut255 = c->lut255.p;
     a.att = c->att.p;
     a.partial = c->partial.p;
     a.counters = c->scratch.p;
@@ -1436,6 +1480,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->leaf_visits = h[zrt::kLeaves];
     out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
     out->wide_nodes = c->n_wide;
+    out->texel_bytes = c->texel_bytes;
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
     out->preprocess_ms = c->preprocess_ms;
