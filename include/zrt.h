@@ -165,7 +165,12 @@ typedef struct zrt_params {
  * counts BVH node visits, primitive tests, shaded hits and texel fetches
  * (zrt_stats).  Images are identical; the default flavour counts only the
  * Progress counters (raytrace.zig:20-34). */
-enum { ZRT_FLAG_STATS = 1u };
+enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u };
+/* Scheduling (FAST traversal, spp >= 128, unless ZRT_FLAG_NO_SCHEDULE): a probe
+ * launch renders 4 samples per pixel of every tile (results discarded) and
+ * records each tile's cost; the tiles are radix-sorted by descending cost on
+ * the device and the render launch hands out units costliest first, so no long
+ * unit starts at the end of the launch.  Images do not depend on it. */
 
 /* Progress counters (raytrace.zig:20-34) + timings. */
 typedef struct zrt_stats {
@@ -183,7 +188,7 @@ typedef struct zrt_stats {
   uint64_t leaf_visits;   /* FAST traversal: reference leaf boxes tested (node_visits = wide nodes) */
   double preprocess_ms;   /* BVH build + flatten (raytrace.zig:150) */
   double upload_ms;
-  double render_ms;       /* kernel time (HIP events) */
+  double render_ms;       /* device time of the sampling loop: schedule probe + sort + render kernel */
   double gather_ms;
   uint32_t used_bvh;      /* preprocessSufraces decision (raytrace.zig:124-133) */
   uint32_t bvh_nodes;
@@ -193,7 +198,7 @@ typedef struct zrt_stats {
   uint32_t wide_nodes;    /* FAST traversal: 4-wide nodes over the reference leaves */
   uint32_t texel_bytes;   /* bytes per texel on the device: 4 when every image is exact 8-bit
                              (c == k/255, png_image.zig:76-89), else 12 (f32 RGB); 0: no images */
-  uint32_t reserved_stats;
+  float schedule_ms;       /* probe + sort before the render launch (included in render_ms) */
 } zrt_stats;
 
 /* ---- entry points -------------------------------------------------------- */

@@ -279,3 +279,18 @@ def test_eight_bit_texels_selected(scenes):
     p = z.RenderParams(8, 8, 1, 2)
     _, gs = z.render(scenes(4), scenes(4).camera, p)
     assert gs["texel_bytes"] == 4  # earthmap from png_image.zig's byte / 255
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_schedule_bit_exact(scenes, world):
+    """The longest-first tile schedule (probe + device sort, spp >= 128) only
+    reorders work: the frame equals the unscheduled one and the oracle's."""
+    s = scenes(2)
+    p = z.RenderParams(24, 24, 128, 6)
+    ref, rs = O.render(s.view, s.camera, p)
+    sched = render_partitioned(s, p, world)
+    plain = render_partitioned(s, z.RenderParams(24, 24, 128, 6, flags=z.ZRT_FLAG_NO_SCHEDULE), world)
+    assert_bit_exact(sched, ref)
+    assert_bit_exact(plain, ref)
+    gpu, gs = z.render(s, s.camera, p)
+    assert gs["schedule_ms"] > 0 and gs["rays_processed"] == rs["rays_processed"]

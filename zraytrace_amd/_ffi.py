@@ -30,6 +30,7 @@ ZRT_RNG_COUNTER, ZRT_RNG_REFERENCE_STREAM = 0, 1
 ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256 = 0, 1
 ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE, ZRT_TRAVERSAL_BINARY = 0, 1, 2
 ZRT_FLAG_STATS = 1
+ZRT_FLAG_NO_SCHEDULE = 2
 
 
 class Vec3(C.Structure):
@@ -90,7 +91,7 @@ class Stats(C.Structure):
                 ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),
                 ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32),
                 ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32),
-                ("texel_bytes", C.c_uint32), ("reserved_stats", C.c_uint32)]
+                ("texel_bytes", C.c_uint32), ("schedule_ms", C.c_float)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -22,6 +22,7 @@
 //   * RNG: one Xoroshiro128+ (or Xoshiro256++) stream per (pixel, sample),
 //     seeded through SplitMix64 exactly as DefaultPrng.init seeds.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -69,6 +70,8 @@ struct KArgs {
   float4* __restrict__ att;            // [max_depth][n_lanes]
   float4* __restrict__ partial;        // [tile slot][chunk] chunk sums
   uint32_t* __restrict__ work_counter;
+  uint32_t* __restrict__ unit_cost;         // probe: loop iterations a wave spent on each tile, else null
+  const uint32_t* __restrict__ tile_order;  // local tiles in the order units are handed out, or null
   unsigned long long* __restrict__ counters;  // kNumCounters x u64
   uint32_t* __restrict__ error_flag;
   float org[3], llc[3], hor[3], ver[3];
@@ -605,17 +608,17 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
 constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 
-// StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
-// more blocks fit per CU), uint32_t otherwise.
-template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
 #ifndef ZRT_WAVES_PER_SIMD
 #define ZRT_WAVES_PER_SIMD 8  // binary/reference/list; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
 #endif
 #ifndef ZRT_WAVES_WIDE
 #define ZRT_WAVES_WIDE 6      // FAST (wide tree) kernel; A/B: w4 15.2, w5 16.6, w6 17.3, w7 17.3 Gray/s
 #endif
-__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
-    render_kernel(const KArgs a) {
+
+// StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
+// more blocks fit per CU), uint32_t otherwise.
+template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
+__device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   const int lane = (int)__lane_id();
@@ -624,6 +627,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
   bool active = false, in_sample = false;  // active: this lane still has samples in the wave's unit
   uint32_t px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
   uint32_t gate = 0, unit_end = 0;  // wave-uniform: lanes run samples < gate; the unit ends at unit_end
+  uint32_t cur_lt = 0xffffffffu, iters = 0;  // wave-uniform: the unit's tile, loop iterations spent on it
   uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -635,6 +639,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
 
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
   for (;;) {
+    ++iters;
     uint64_t t0 = prof_stamp();
     // ---- work: the WAVE takes units (local tile lt, a group of unit_chunks
     // chunks) from the global counter, one atomic per unit; lane p renders
@@ -647,11 +652,15 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
       if (__ballot(active) != 0ull) {
         gate = min(gate + a.sync, unit_end);
       } else {
+        if (a.unit_cost && cur_lt != 0xffffffffu && lane == 0) a.unit_cost[cur_lt] = iters;
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.work_counter, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= a.total_work) break;  // the counter is exhausted
-        const uint32_t lt = u / a.n_groups, g = u - lt * a.n_groups;
+        const uint32_t ord = u / a.n_groups, g = u - ord * a.n_groups;
+        const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;  // costliest tiles first
+        cur_lt = lt;
+        iters = 0;
         const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
         px = (t % a.tiles_x) * 8u + ((uint32_t)lane & 7u);
         py = (t / a.tiles_x) * 8u + ((uint32_t)lane >> 3);
@@ -852,6 +861,20 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES
     wave_add_u64(&a.counters[kTexels], c_tex);
     wave_add_u64(&a.counters[kLeaves], c_leaves);
   }
+}
+
+template <int MODE, int PRNG, bool STATS, class StackT>
+__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
+    render_kernel(const KArgs a) {
+  render_loop<MODE, PRNG, STATS, StackT>(a);
+}
+
+// The scheduling probe (FAST traversal): the same loop over a few samples per
+// pixel, one unit per tile, recording each tile's cost (a.unit_cost); its own
+// symbol so profiles keep it apart from the render launches.
+template <int PRNG, class StackT>
+__global__ void __launch_bounds__(kBlock, ZRT_WAVES_WIDE) schedule_probe_kernel(const KArgs a) {
+  render_loop<3, PRNG, false, StackT>(a);
 }
 
 // Per-pixel sum of the chunk sums in chunk order, times 1/spp
@@ -1069,7 +1092,14 @@ struct zrt_ctx {
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
   zrt::DevBuf<float4> partial;
   zrt::DevBuf<uint32_t> rank_base;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // scheduling probe: its own partial sums + counters, per-tile costs, the sort
+  zrt::DevBuf<float4> probe_partial;
+  zrt::DevBuf<unsigned long long> probe_scratch;
+  zrt::DevBuf<uint32_t> tile_cost, tile_ids, cost_sorted, tile_order;
+  zrt::DevBuf<uint8_t> sort_temp;
+  uint32_t tile_ids_n = 0;
+  bool scheduled = false;
+  hipEvent_t ev_pre = nullptr, ev0 = nullptr, ev1 = nullptr;
   double preprocess_ms = 0, upload_ms = 0;
   // last launch
   uint32_t last_pixels = 0, last_spp = 0, launched = 0;
@@ -1077,6 +1107,7 @@ struct zrt_ctx {
   int last_mode = 0;
   int cu_count = 0;
   ~zrt_ctx() {
+    if (ev_pre) (void)hipEventDestroy(ev_pre);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1271,6 +1302,62 @@ void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
                : select_kernel_ps<ZRT_PRNG_XOROSHIRO128, false>(mode, stk16);
 }
 
+template <int PRNG>
+void* probe_ptr(bool stk16) {
+  return stk16 ? reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint16_t>)
+               : reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint32_t>);
+}
+
+// Longest-processing-time-first order of this rank's tiles (zrt.h,
+// ZRT_FLAG_NO_SCHEDULE): the probe renders kProbeSpp samples of every tile as
+// one unit each and records the loop iterations its wave spent (lockstep makes
+// that the unit's time); a stable device radix sort orders the tiles by
+// descending cost, ties in tile order.  Sets a.tile_order for the render launch.
+void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my_tiles, uint32_t grid,
+                    size_t lds, hipStream_t st) {
+  constexpr uint32_t kProbeSpp = 4;
+  KArgs pa = a;
+  pa.spp = kProbeSpp;
+  pa.chunk = kProbeSpp;
+  pa.n_chunks = 1;
+  pa.unit_chunks = 1;
+  pa.n_groups = 1;
+  pa.total_work = my_tiles;
+  if (c->probe_partial.n < uint64_t(my_tiles) * 64u) c->probe_partial.alloc(uint64_t(my_tiles) * 64u);
+  if (c->probe_scratch.n < uint64_t(kScratchSlots)) c->probe_scratch.alloc(kScratchSlots);
+  if (c->tile_cost.n < my_tiles) {
+    c->tile_cost.alloc(my_tiles);
+    c->cost_sorted.alloc(my_tiles);
+    c->tile_order.alloc(my_tiles);
+  }
+  if (c->tile_ids_n != my_tiles) {
+    std::vector<uint32_t> ids(my_tiles);
+    for (uint32_t i = 0; i < my_tiles; ++i) ids[i] = i;
+    c->tile_ids.upload(ids);
+    c->tile_ids_n = my_tiles;
+  }
+  pa.partial = c->probe_partial.p;
+  pa.counters = c->probe_scratch.p;
+  pa.work_counter = reinterpret_cast<uint32_t*>(c->probe_scratch.p + kWorkSlot);
+  pa.error_flag = reinterpret_cast<uint32_t*>(c->probe_scratch.p + kErrorSlot);
+  pa.unit_cost = c->tile_cost.p;
+  pa.tile_order = nullptr;
+  const uint32_t pgrid = std::max(1u, std::min(grid, (my_tiles + kBlock / 64 - 1) / (kBlock / 64)));
+  pa.n_lanes = pgrid * kBlock;
+  HIPCHK(hipMemsetAsync(c->probe_scratch.p, 0, kScratchSlots * sizeof(unsigned long long), st));
+  void* fn = prng == ZRT_PRNG_XOSHIRO256 ? probe_ptr<ZRT_PRNG_XOSHIRO256>(stk16)
+                                         : probe_ptr<ZRT_PRNG_XOROSHIRO128>(stk16);
+  void* args[] = {&pa};
+  HIPCHK(hipLaunchKernel(fn, dim3(pgrid), dim3(kBlock), args, lds, st));
+  size_t bytes = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, c->tile_cost.p, c->cost_sorted.p,
+                                                      c->tile_ids.p, c->tile_order.p, int(my_tiles), 0, 32, st));
+  if (c->sort_temp.n < bytes) c->sort_temp.alloc(bytes);
+  HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(c->sort_temp.p, bytes, c->tile_cost.p, c->cost_sorted.p,
+                                                      c->tile_ids.p, c->tile_order.p, int(my_tiles), 0, 32, st));
+  a.tile_order = c->tile_order.p;
+}
+
 int hip_fail(const HipError& e) {
   return fail(ZRT_E_HIP, e.where + ": " + hipGetErrorString(e.err));
 }
@@ -1301,6 +1388,7 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
     c->device = int(params->device);
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev_pre));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     hipDeviceProp_t prop;
@@ -1423,6 +1511,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_groups = n_groups;
     a.sync = ZRT_SYNC_SAMPLES;
 
+    HIPCHK(hipEventRecord(c->ev_pre, st));
+    const bool schedule =
+        mode == 3 && !(p->flags & ZRT_FLAG_NO_SCHEDULE) && p->samples_per_pixel >= 128 && my_tiles >= 2;
+    c->scheduled = schedule;
+    if (schedule) zrt::schedule_tiles(c, a, p->prng, stk16, my_tiles, grid, lds, st);
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
       void* args[] = {&a};
@@ -1485,9 +1578,11 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
     out->preprocess_ms = c->preprocess_ms;
     out->upload_ms = c->upload_ms;
-    float ms = 0.0f;
-    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    float ms = 0.0f, sched = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_pre, c->ev1));
+    HIPCHK(hipEventElapsedTime(&sched, c->ev_pre, c->ev0));
     out->render_ms = ms;
+    out->schedule_ms = c->scheduled ? sched : 0.0f;
     out->used_bvh = c->use_bvh ? 1 : 0;
     out->bvh_nodes = c->n_nodes;
     out->bvh_max_depth = c->bvh_depth;
