@@ -19,14 +19,32 @@ buf = torch.empty(ctx.tile_count(full) * 64 * 3, device="cuda")
 ctx.render_tiles(s.camera, full, buf.data_ptr(), stream)
 ctx.render_tiles(s.camera, full, buf.data_ptr(), stream)
 t1 = ctx.kernel_ms()
-per = []
+per, sched, total = [], [], []
 for r in range(world):
     p = z.RenderParams(w, h, spp, depth, rank=r, world_size=world)
     ctx.render_tiles(s.camera, p, buf.data_ptr(), stream)
     per.append(ctx.kernel_ms())
+    st = ctx.stats()
+    sched.append(st["schedule_ms"])
+    total.append(st["render_ms"])
 print(f"1 GPU: {t1:.1f} ms; {world} ranks: {', '.join(f'{x:.1f}' for x in per)} ms; "
       f"ideal {t1 / world:.1f}, max {max(per):.1f} -> kernel efficiency {t1 / world / max(per):.3f}; "
-      f"tiles {tile_counts(z.RenderParams(w, h, spp, depth, world_size=world))[:2]}")
+      f"tiles {tile_counts(z.RenderParams(w, h, spp, depth, world_size=world))[:2]}; "
+      f"schedule ms {max(sched):.2f}; max render_ms (probe + sort + kernel) {max(total):.2f}")
+if len(sys.argv) > 7:
+    import numpy as np
+    p = z.RenderParams(w, h, spp, depth, rank=world - 1, world_size=world)
+    ctx.render_tiles(s.camera, p, buf.data_ptr(), stream)
+    costs, order = ctx.debug_schedule()
+    c = np.sort(costs.astype(np.float64))[::-1]
+    n_groups = (spp + 63) // 64
+    waves = 6144
+    # probe iterations cover 4 samples; a unit covers 64 (one chunk)
+    unit = c * 16
+    print(f"probe costs (iterations / 4 spp): mean {c.mean():.1f}, p50 {np.median(c):.0f}, p99 {c[len(c) // 100]:.0f}, "
+          f"max {c[0]:.0f}; top {c[:6].astype(int).tolist()}; per-wave unit budget {unit.sum() * n_groups / waves:.0f} "
+          f"vs largest unit {unit[0]:.0f} iterations")
+    sys.exit(0)
 rays = []
 for r in range(world):
     p = z.RenderParams(w, h, spp, depth, rank=r, world_size=world)
