@@ -259,6 +259,15 @@ int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
  * [16..20] per-section cycle sums of ZRT_PROFILE builds. */
 int zrt_ctx_debug_counters(zrt_ctx* ctx, uint64_t* out, uint32_t n);
 
+/* The last launch's schedule (diagnostics): per local tile, the probe's cost
+ * (loop iterations its wave spent on 4 samples per pixel), and the tile order
+ * the render launch used.  *n_tiles = 0 when the launch was not scheduled. */
+int zrt_ctx_debug_schedule(zrt_ctx* ctx, uint32_t* costs, uint32_t* order, uint32_t cap, uint32_t* n_tiles);
+
+/* ZRT_PROFILE builds only (diagnostics): {start, end} s_memrealtime stamps
+ * (100 MHz) of every wave of the last render launch; *n_waves = 0 otherwise. */
+int zrt_ctx_debug_wave_times(zrt_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n_waves);
+
 /* Duration in ms of the last zrt_ctx_render_tiles' kernel (HIP events on the
  * launch stream; synchronises). */
 int zrt_ctx_last_kernel_ms(zrt_ctx* ctx, double* ms);

@@ -153,6 +153,22 @@ class RenderContext:
         check(lib().zrt_ctx_debug_counters(self._h, out, n))
         return list(out)
 
+    def debug_wave_times(self, cap: int = 1 << 16):
+        """ZRT_PROFILE builds: array[n_waves, 2] of (start, end) 100 MHz stamps of the last launch."""
+        out = np.zeros(cap, np.uint64)
+        n = C.c_uint32()
+        check(lib().zrt_ctx_debug_wave_times(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(n)))
+        return out[: 2 * n.value].reshape(-1, 2).copy()
+
+    def debug_schedule(self, cap: int = 1 << 20):
+        """(probe cost per local tile, tile order) of the last launch; empty if unscheduled."""
+        costs = np.zeros(cap, np.uint32)
+        order = np.zeros(cap, np.uint32)
+        n = C.c_uint32()
+        check(lib().zrt_ctx_debug_schedule(self._h, costs.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                           order.ctypes.data_as(C.POINTER(C.c_uint32)), cap, C.byref(n)))
+        return costs[: n.value].copy(), order[: n.value].copy()
+
     def kernel_ms(self) -> float:
         ms = C.c_double()
         check(lib().zrt_ctx_last_kernel_ms(self._h, C.byref(ms)))

@@ -120,6 +120,9 @@ SIGNATURES = [
     ("zrt_ctx_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("zrt_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("zrt_ctx_debug_counters", C.c_int, [_P, C.POINTER(C.c_uint64), C.c_uint32]),
+    ("zrt_ctx_debug_wave_times", C.c_int, [_P, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("zrt_ctx_debug_schedule", C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32,
+                                         C.POINTER(C.c_uint32)]),
     ("zrt_scene_load", C.c_int, [C.c_uint32, C.c_char_p, C.POINTER(_P), C.POINTER(Camera)]),
     ("zrt_scene_view", C.POINTER(Scene), [_P]),
     ("zrt_scene_free", None, [_P]),

@@ -72,6 +72,7 @@ struct KArgs {
   uint32_t* __restrict__ work_counter;
   uint32_t* __restrict__ unit_cost;         // probe: loop iterations a wave spent on each tile, else null
   const uint32_t* __restrict__ tile_order;  // local tiles in the order units are handed out, or null
+  unsigned long long* __restrict__ wave_times;  // ZRT_PROFILE builds: {start, end} realtime per wave
   unsigned long long* __restrict__ counters;  // kNumCounters x u64
   uint32_t* __restrict__ error_flag;
   float org[3], llc[3], hor[3], ver[3];
@@ -106,6 +107,9 @@ __device__ __forceinline__ uint64_t prof_stamp() {
 constexpr int kBlock = 256;
 #ifndef ZRT_UNIT_CHUNKS
 #define ZRT_UNIT_CHUNKS 1  // chunks of one pixel per work unit (a unit = 8x8 tile x this many chunks)
+#endif
+#ifndef ZRT_PROBE_SPP
+#define ZRT_PROBE_SPP 4  // samples per pixel of the scheduling probe
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -628,6 +632,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   uint32_t px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
   uint32_t gate = 0, unit_end = 0;  // wave-uniform: lanes run samples < gate; the unit ends at unit_end
   uint32_t cur_lt = 0xffffffffu, iters = 0;  // wave-uniform: the unit's tile, loop iterations spent on it
+  const uint64_t t_begin = ZRT_PROFILE ? __builtin_amdgcn_s_memrealtime() : 0;
   uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -846,8 +851,14 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
   }
-  if (ZRT_PROFILE && lane == 0)
+  if (ZRT_PROFILE && lane == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(&a.counters[kProfSlot + k], (unsigned long long)pf[k]);
+    if (a.wave_times) {
+      const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+      a.wave_times[2 * w] = t_begin;
+      a.wave_times[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 
   wave_add_u64(&a.counters[kDepthHits], c_depth);
   wave_add_u64(&a.counters[kReflections], c_refl);
@@ -1098,6 +1109,8 @@ struct zrt_ctx {
   zrt::DevBuf<uint32_t> tile_cost, tile_ids, cost_sorted, tile_order;
   zrt::DevBuf<uint8_t> sort_temp;
   uint32_t tile_ids_n = 0;
+  zrt::DevBuf<unsigned long long> wave_times;  // ZRT_PROFILE builds
+  uint32_t n_waves = 0;
   bool scheduled = false;
   hipEvent_t ev_pre = nullptr, ev0 = nullptr, ev1 = nullptr;
   double preprocess_ms = 0, upload_ms = 0;
@@ -1315,7 +1328,7 @@ void* probe_ptr(bool stk16) {
 // descending cost, ties in tile order.  Sets a.tile_order for the render launch.
 void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my_tiles, uint32_t grid,
                     size_t lds, hipStream_t st) {
-  constexpr uint32_t kProbeSpp = 4;
+  constexpr uint32_t kProbeSpp = ZRT_PROBE_SPP;
   KArgs pa = a;
   pa.spp = kProbeSpp;
   pa.chunk = kProbeSpp;
@@ -1516,6 +1529,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
         mode == 3 && !(p->flags & ZRT_FLAG_NO_SCHEDULE) && p->samples_per_pixel >= 128 && my_tiles >= 2;
     c->scheduled = schedule;
     if (schedule) zrt::schedule_tiles(c, a, p->prng, stk16, my_tiles, grid, lds, st);
+    if (ZRT_PROFILE) {
+      c->n_waves = grid * (zrt::kBlock / 64);
+      if (c->wave_times.n < 2ull * c->n_waves) c->wave_times.alloc(2ull * c->n_waves);
+      a.wave_times = c->wave_times.p;
+    }
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
       void* args[] = {&a};
@@ -1603,6 +1621,36 @@ int zrt_ctx_debug_counters(zrt_ctx* c, uint64_t* out, uint32_t n) {
     unsigned long long h[zrt::kScratchSlots] = {0};
     HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < n && i < uint32_t(zrt::kScratchSlots); ++i) out[i] = h[i];
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_debug_wave_times(zrt_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n_waves) {
+  if (!c || !n_waves) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *n_waves = ZRT_PROFILE ? c->n_waves : 0u;
+    const size_t n = std::min<size_t>(cap / 2, *n_waves);
+    if (n && out) HIPCHK(hipMemcpy(out, c->wave_times.p, 2 * n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  }
+}
+
+int zrt_ctx_debug_schedule(zrt_ctx* c, uint32_t* costs, uint32_t* order, uint32_t cap, uint32_t* n_tiles) {
+  if (!c || !n_tiles) return fail(ZRT_E_INVALID, "null argument");
+  if (!c->launched) return fail(ZRT_E_INVALID, "no kernel launched on this context yet");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *n_tiles = c->scheduled ? c->tile_ids_n : 0u;
+    const size_t n = std::min<size_t>(cap, *n_tiles);
+    if (n && costs) HIPCHK(hipMemcpy(costs, c->tile_cost.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (n && order) HIPCHK(hipMemcpy(order, c->tile_order.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
