@@ -167,7 +167,7 @@ typedef struct zrt_params {
  * Progress counters (raytrace.zig:20-34). */
 enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u };
 /* Scheduling (FAST traversal, spp >= 128, unless ZRT_FLAG_NO_SCHEDULE): a probe
- * launch renders 4 samples per pixel of every tile (results discarded) and
+ * launch renders 1 sample per pixel of every tile (results discarded) and
  * records each tile's cost; the tiles are radix-sorted by descending cost on
  * the device and the render launch hands out units costliest first, so no long
  * unit starts at the end of the launch.  Images do not depend on it. */
@@ -260,7 +260,7 @@ int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
 int zrt_ctx_debug_counters(zrt_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* The last launch's schedule (diagnostics): per local tile, the probe's cost
- * (loop iterations its wave spent on 4 samples per pixel), and the tile order
+ * (loop iterations its wave spent on ZRT_PROBE_SPP samples per pixel), and the tile order
  * the render launch used.  *n_tiles = 0 when the launch was not scheduled. */
 int zrt_ctx_debug_schedule(zrt_ctx* ctx, uint32_t* costs, uint32_t* order, uint32_t cap, uint32_t* n_tiles);
 

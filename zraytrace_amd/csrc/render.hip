@@ -109,7 +109,7 @@ constexpr int kBlock = 256;
 #define ZRT_UNIT_CHUNKS 1  // chunks of one pixel per work unit (a unit = 8x8 tile x this many chunks)
 #endif
 #ifndef ZRT_PROBE_SPP
-#define ZRT_PROBE_SPP 4  // samples per pixel of the scheduling probe
+#define ZRT_PROBE_SPP 1  // samples per pixel of the scheduling probe; A/B at N=8: 1, 2, 4, 8 give the same render launch
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
