@@ -185,7 +185,7 @@ def main():
         frame_sha1 = hashlib.sha1(frame.cpu().numpy().tobytes()).hexdigest()
         value = total_rays * args.steps / elapsed / 1e6
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        chunk = args.chunk or 64
+        chunk = args.chunk or 32  # ZRT_DEFAULT_SAMPLE_CHUNK
         n_units = my_tiles * 64 * ((args.spp + chunk - 1) // chunk)
         algo = algorithmic_bytes(diag, n_units, diag["pixels_processed"])
         achieved = algo / avg_kernel_s / 1e9

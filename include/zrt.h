@@ -153,9 +153,10 @@ typedef struct zrt_params {
   uint32_t device;                   /* HIP device ordinal */
   /* COUNTER mode: a pixel's samples are summed in chunks of sample_chunk
    * consecutive samples (each chunk sequentially, as raytrace.zig:177 does),
-   * and the chunk sums are then added in chunk order.  0 selects 64.  With
-   * sample_chunk >= samples_per_pixel this is the reference's single
-   * sequential sum.  A chunk is the kernel's unit of work. */
+   * and the chunk sums are then added in chunk order.  0 selects 32
+   * (ZRT_DEFAULT_SAMPLE_CHUNK).  With sample_chunk >= samples_per_pixel this is
+   * the reference's single sequential sum.  A chunk is the kernel's unit of
+   * work: shorter units end a launch sooner. */
   uint32_t sample_chunk;
   uint32_t flags;                    /* ZRT_FLAG_* */
   uint32_t reserved;
@@ -166,6 +167,7 @@ typedef struct zrt_params {
  * (zrt_stats).  Images are identical; the default flavour counts only the
  * Progress counters (raytrace.zig:20-34). */
 enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u };
+enum { ZRT_DEFAULT_SAMPLE_CHUNK = 32u };
 /* Scheduling (FAST traversal, spp >= 128, unless ZRT_FLAG_NO_SCHEDULE): a probe
  * launch renders 1 sample per pixel of every tile (results discarded) and
  * records each tile's cost; the tiles are radix-sorted by descending cost on

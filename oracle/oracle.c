@@ -629,7 +629,7 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
   const float f_width = (float)p->width;
   const float f_height = (float)p->height;
   const float color_scale = 1.0f / (float)p->samples_per_pixel;
-  const uint32_t chunk = p->sample_chunk ? p->sample_chunk : 64;
+  const uint32_t chunk = p->sample_chunk ? p->sample_chunk : ZRT_DEFAULT_SAMPLE_CHUNK;
   for (uint32_t y = y0; y < y1; ++y) {
     const float f_y = (float)y;
     for (uint32_t x = 0; x < p->height; ++x) {  /* raytrace.zig:168 bound */

@@ -11,7 +11,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEFAULT = {"scene": 2, "width": 2048, "height": 2048, "spp": 1024, "max_depth": 20, "traversal": "fast",
-           "sample_chunk": 64}
+           "sample_chunk": 32}
 
 
 def main():

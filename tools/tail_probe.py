@@ -10,10 +10,11 @@ import zraytrace_amd as z
 from zraytrace_amd.dist import tile_counts
 
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+chunk = int(os.environ.get("ZRT_CHUNK", "0"))
 scene, w, h, spp, depth = (int(x) for x in (sys.argv[2:7] if len(sys.argv) > 6 else (2, 2048, 2048, 1024, 20)))
 s = z.load_scene(scene)
 stream = torch.cuda.current_stream().cuda_stream
-full = z.RenderParams(w, h, spp, depth)
+full = z.RenderParams(w, h, spp, depth, sample_chunk=chunk)
 ctx = z.RenderContext(s, full)
 buf = torch.empty(ctx.tile_count(full) * 64 * 3, device="cuda")
 ctx.render_tiles(s.camera, full, buf.data_ptr(), stream)
@@ -21,7 +22,7 @@ ctx.render_tiles(s.camera, full, buf.data_ptr(), stream)
 t1 = ctx.kernel_ms()
 per, sched, total = [], [], []
 for r in range(world):
-    p = z.RenderParams(w, h, spp, depth, rank=r, world_size=world)
+    p = z.RenderParams(w, h, spp, depth, rank=r, world_size=world, sample_chunk=chunk)
     ctx.render_tiles(s.camera, p, buf.data_ptr(), stream)
     per.append(ctx.kernel_ms())
     st = ctx.stats()

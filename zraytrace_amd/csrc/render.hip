@@ -1462,7 +1462,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
     uint32_t grid = uint32_t(c->cu_count) * uint32_t(per_cu);
-    const uint32_t chunk = p->sample_chunk ? p->sample_chunk : 64u;
+    const uint32_t chunk = p->sample_chunk ? p->sample_chunk : ZRT_DEFAULT_SAMPLE_CHUNK;
     const uint32_t n_chunks = (p->samples_per_pixel + chunk - 1) / chunk;
     const uint32_t unit_chunks = ZRT_UNIT_CHUNKS;
     const uint32_t n_groups = (n_chunks + unit_chunks - 1) / unit_chunks;
