@@ -68,7 +68,7 @@ struct KArgs {
   const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
   const float* __restrict__ lut255;      // k / 255.0f for k = 0..255 (png_image.zig:88)
   float4* __restrict__ att;            // [max_depth][n_lanes]
-  float4* __restrict__ partial;        // [tile slot][chunk] chunk sums
+  float4* __restrict__ partial;        // [chunk][tile slot] chunk sums
   uint32_t* __restrict__ work_counter;
   uint32_t* __restrict__ unit_cost;         // probe: loop iterations a wave spent on each tile, else null
   const uint32_t* __restrict__ tile_order;  // local tiles in the order units are handed out, or null
@@ -81,6 +81,7 @@ struct KArgs {
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
   uint32_t chunk, n_chunks, unit_chunks, n_groups, sync;
+  uint32_t n_slots;  // this launch's pixel slots (tiles x 64): the stride of a chunk in partial
   unsigned long long seed_mix;
 };
 
@@ -674,7 +675,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         unit_end = min(min(chunk_j + a.unit_chunks, a.n_chunks) * a.chunk, a.spp);
         gate = min(sample + a.sync, unit_end);
         active = px < a.xbound && py < a.height;  // else: finalize writes black
-        slot = (lt * 64u + (uint32_t)lane) * a.n_chunks + chunk_j;
+        slot = chunk_j * a.n_slots + lt * 64u + (uint32_t)lane;  // partial is [chunk][pixel slot]
         sample_end = min(sample + a.chunk, a.spp);
         acc_r = acc_g = acc_b = 0.0f;
         in_sample = false;
@@ -843,7 +844,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       in_sample = false;
       if (++sample == sample_end) {  // chunk done: its sequential sum
         a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
-        ++slot;
+        slot += a.n_slots;
         sample_end = min(sample + a.chunk, a.spp);
         acc_r = acc_g = acc_b = 0.0f;
         active = sample < unit_end;
@@ -901,9 +902,8 @@ __global__ void finalize_kernel(const float4* __restrict__ partial, float* __res
   const uint32_t py = (t / tiles_x) * 8u + (p >> 3);
   float r = 0.0f, g = 0.0f, b = 0.0f;
   if (px < xbound && py < height) {
-    const float4* q = partial + (size_t)i * n_chunks;
-    for (uint32_t j = 0; j < n_chunks; ++j) {
-      const float4 v = q[j];
+    for (uint32_t j = 0; j < n_chunks; ++j) {  // [chunk][slot]: a wave reads 1 KiB per chunk
+      const float4 v = partial[(size_t)j * n_slots + i];
       r += v.x;
       g += v.y;
       b += v.z;
@@ -1523,6 +1523,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.unit_chunks = unit_chunks;
     a.n_groups = n_groups;
     a.sync = ZRT_SYNC_SAMPLES;
+    a.n_slots = my_tiles * 64u;
 
     HIPCHK(hipEventRecord(c->ev_pre, st));
     const bool schedule =
