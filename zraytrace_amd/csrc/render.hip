@@ -80,8 +80,9 @@ struct KArgs {
   uint32_t width, height, xbound, spp, max_depth;
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
-  uint32_t chunk, n_chunks, unit_chunks, n_groups, sync;
+  uint32_t chunk, n_chunks, sync;  // a work unit = one chunk of one tile
   uint32_t n_slots;  // this launch's pixel slots (tiles x 64): the stride of a chunk in partial
+  uint32_t wide_stride;  // float4s per octant copy of the wide tree (ZRT_OCT)
   unsigned long long seed_mix;
 };
 
@@ -106,11 +107,14 @@ __device__ __forceinline__ uint64_t prof_stamp() {
 }
 
 constexpr int kBlock = 256;
-#ifndef ZRT_UNIT_CHUNKS
-#define ZRT_UNIT_CHUNKS 1  // chunks of one pixel per work unit (a unit = 8x8 tile x this many chunks)
-#endif
 #ifndef ZRT_PROBE_SPP
 #define ZRT_PROBE_SPP 1  // samples per pixel of the scheduling probe; A/B at N=8: 1, 2, 4, 8 give the same render launch
+#endif
+#ifndef ZRT_OCT
+#define ZRT_OCT 1  // wide tree stored once per ray octant (near / far planes pre-swapped)
+#endif
+#ifndef ZRT_OCT_COPIES
+#define ZRT_OCT_COPIES 1  // ZRT_OCT: the eight octant copies in HBM (0: one copy, planes selected per ray)
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -436,6 +440,174 @@ __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   ra = tr;
 }
 
+#if ZRT_OCT
+// Two slots' slab distances (bound - o) * inv.  (Written as packed f32,
+// v_pk_add_f32 / v_pk_mul_f32 with the same roundings, this traversal ran
+// 1.2-1.8x slower: packed f32 issues at half the rate of single f32 here.)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 slab2(float b0, float b1, float o, float inv) {
+  return (f2){(b0 - o) * inv, (b1 - o) * inv};
+}
+
+struct SlotT {
+  float en, ex;
+};
+__device__ __forceinline__ SlotT slot_interval(float nx, float ny, float nz, float fx, float fy, float fz,
+                                               float tb) {
+  const float t_min = 0.001f;
+  SlotT s;
+  s.en = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, t_min));
+  s.ex = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tb));
+  return s;
+}
+// The reference's own loose test (aabb.zig:109-127) of leaf slot k whose
+// narrowed test passed with en >= ex (rare; with en < ex it passes outright:
+// an <= en < ex <= ax on every axis): each axis on its own, its distances
+// recomputed from the node in memory (the same two roundings as the packed
+// form) so that none of them stays live across the node.
+__device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, const RayT& r, float tb,
+                                           bool sx, bool sy, bool sz) {
+  const float t_min = 0.001f;
+  const float* f = reinterpret_cast<const float*>(q) + k;
+#if ZRT_OCT_COPIES
+  (void)sx; (void)sy; (void)sz;
+  const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
+#else
+  const int px = sx ? 12 : 0, py = sy ? 16 : 4, pz = sz ? 20 : 8;
+  const int qx = sx ? 0 : 12, qy = sy ? 4 : 16, qz = sz ? 8 : 20;
+#endif
+  const float nx = (f[px] - r.ox) * r.ix, fx = (f[qx] - r.ox) * r.ix;
+  const float ny = (f[py] - r.oy) * r.iy, fy = (f[qy] - r.oy) * r.iy;
+  const float nz = (f[pz] - r.oz) * r.iz, fz = (f[qz] - r.oz) * r.iz;
+  return (__builtin_fminf(fx, tb) > __builtin_fmaxf(nx, t_min)) &&
+         (__builtin_fminf(fy, tb) > __builtin_fmaxf(ny, t_min)) &&
+         (__builtin_fminf(fz, tb) > __builtin_fmaxf(nz, t_min));
+}
+
+// FAST: near-first over the 4-wide tree (accel_build.cpp), stored once per
+// ray octant with each axis' min / max planes swapped where the octant's
+// direction is negative, so a node's first three float4 are the four slots'
+// near planes and the next three their far planes: the reference's swap
+// (aabb.zig:116-118) is done by the layout, not per slot.  All four slots are
+// tested against the t_max at node entry (a leaf passing with a t_max >= the
+// current one is a superset of what the reference opens, and every primitive
+// test still uses the current best with lower-slot tie-breaking); leaf slots
+// are intersected in place, inner slots are sorted by entry distance and the
+// farther ones pushed, branch-free.
+template <bool STATS, class StackT>
+__device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
+                                              float& best_t, int& best, uint32_t& c_nodes, uint32_t& c_leaves,
+                                              uint32_t& c_tri, uint32_t& c_sph) {
+  const int stride = kBlock;
+  const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
+  const float inf = __builtin_inff();
+  const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
+#if ZRT_OCT_COPIES
+  const uint32_t oct = (sx ? 1u : 0u) | (sy ? 2u : 0u) | (sz ? 4u : 0u);
+  const uint32_t base = oct * a.wide_stride;  // float4 offset of this octant's copy (< 2^32)
+#define ZRT_LOAD_NODE(Q)                                                       \
+  nx = Q[0]; ny = Q[1]; nz = Q[2]; fx = Q[3]; fy = Q[4]; fz = Q[5]; ra = Q[6];
+#else
+  const uint32_t base = 0;
+#define ZRT_LOAD_NODE(Q)                                                       \
+  {                                                                            \
+    const float4 m0 = Q[0], m1 = Q[1], m2 = Q[2], m3 = Q[3], m4 = Q[4], m5 = Q[5]; \
+    nx = sx ? m3 : m0; fx = sx ? m0 : m3;                                      \
+    ny = sy ? m4 : m1; fy = sy ? m1 : m4;                                      \
+    nz = sz ? m5 : m2; fz = sz ? m2 : m5;                                      \
+    ra = Q[6];                                                                 \
+  }
+#endif
+  uint32_t sp = 0;
+  const float4* q = a.wnodes + base;  // the root wide node
+  float4 nx, ny, nz, fx, fy, fz, ra;
+  ZRT_LOAD_NODE(q)
+  for (;;) {
+    int r0 = as_int(ra.x), r1 = as_int(ra.y), r2 = as_int(ra.z), r3 = as_int(ra.w);
+    const float tb = best_t * 1.0000153f;
+#define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
+#define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
+#define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
+    const f2 nx01 = ZRT_SLAB_X(nx, x, y), nx23 = ZRT_SLAB_X(nx, z, w);
+    const f2 ny01 = ZRT_SLAB_Y(ny, x, y), ny23 = ZRT_SLAB_Y(ny, z, w);
+    const f2 nz01 = ZRT_SLAB_Z(nz, x, y), nz23 = ZRT_SLAB_Z(nz, z, w);
+    const f2 fx01 = ZRT_SLAB_X(fx, x, y), fx23 = ZRT_SLAB_X(fx, z, w);
+    const f2 fy01 = ZRT_SLAB_Y(fy, x, y), fy23 = ZRT_SLAB_Y(fy, z, w);
+    const f2 fz01 = ZRT_SLAB_Z(fz, x, y), fz23 = ZRT_SLAB_Z(fz, z, w);
+#undef ZRT_SLAB_X
+#undef ZRT_SLAB_Y
+#undef ZRT_SLAB_Z
+    const SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
+    const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
+    const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
+    const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
+    // narrowed test: entry > exit * (1 + 2^-16) culls
+    const bool h0 = !(s0.en > s0.ex * 1.0000153f), h1 = !(s1.en > s1.ex * 1.0000153f);
+    const bool h2 = !(s2.en > s2.ex * 1.0000153f), h3 = !(s3.en > s3.ex * 1.0000153f);
+    if (STATS) {
+      ++c_nodes;
+      c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
+    }
+    // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
+    bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
+    const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
+    const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
+    if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
+      if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
+      if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
+      if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
+      if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
+    }
+    const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
+    const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
+    // inner slots that pass, keyed by entry distance
+    float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
+    float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
+    const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
+    // sort (entry, ref) ascending: 5 compare-exchanges
+    cswap(k0, r0, k1, r1);
+    cswap(k2, r2, k3, r3);
+    cswap(k0, r0, k2, r2);
+    cswap(k1, r1, k3, r3);
+    cswap(k1, r1, k2, r2);
+    int32_t next = -1;
+    if (n != 0) {
+      // push r_{n-1} .. r_1 (farthest first) and continue with the nearest; the
+      // three stores are unconditional (entries above the new top are dead)
+      if (sp + 3 <= cap) {
+        stk[sp * stride] = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1);
+        stk[(sp + 1) * stride] = (StackT)(n == 4 ? r2 : r1);
+        stk[(sp + 2) * stride] = (StackT)r1;
+      } else {
+        atomicOr(a.error_flag, 1u);
+      }
+      sp = min(sp + n - 1, cap - 3);
+      next = r0;
+    } else if (sp != 0) {
+      --sp;
+      next = (int32_t)stk[sp * stride];
+    }
+    if ((l0 | l1 | l2 | l3) != 0) {
+      const float4 rb = leaf_q[7];
+#define ZRT_WIDE_LEAF(L, RB)                                                        \
+  if (L != 0) {                                                                     \
+    const int pb = as_int(RB);                                                      \
+    prim_test<true, STATS>(a.prims, L, r, best_t, best, c_tri, c_sph);              \
+    if (pb != L) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
+  }
+      ZRT_WIDE_LEAF(l0, rb.x)
+      ZRT_WIDE_LEAF(l1, rb.y)
+      ZRT_WIDE_LEAF(l2, rb.z)
+      ZRT_WIDE_LEAF(l3, rb.w)
+#undef ZRT_WIDE_LEAF
+    }
+    if (next < 0) return;
+    q = a.wnodes + (base + 8u * (uint32_t)next);
+    ZRT_LOAD_NODE(q)
+  }
+#undef ZRT_LOAD_NODE
+}
+#else
 // FAST: near-first over the 4-wide tree (accel_build.cpp).  All four slots of
 // a node are tested against the t_max at node entry (a leaf passing with a
 // t_max >= the current one is a superset of what the reference opens, and
@@ -525,6 +697,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     mnx = q[0]; mny = q[1]; mnz = q[2]; mxx = q[3]; mxy = q[4]; mxz = q[5]; ra = q[6];
   }
 }
+#endif  // ZRT_OCT
 
 // ---------------------------------------------------------------------------
 // shading
@@ -617,7 +790,7 @@ constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 #define ZRT_WAVES_PER_SIMD 8  // binary/reference/list; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
 #endif
 #ifndef ZRT_WAVES_WIDE
-#define ZRT_WAVES_WIDE 6      // FAST (wide tree) kernel; A/B: w4 15.2, w5 16.6, w6 17.3, w7 17.3 Gray/s
+#define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B (octant traversal, 96 VGPRs): w4 46.0, w5 50.6, w6 48.2 (spills) Gray/s
 #endif
 
 // StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
@@ -627,17 +800,18 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   const int lane = (int)__lane_id();
-  const uint64_t gl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;  // n_lanes < 2^32
 
   bool active = false, in_sample = false;  // active: this lane still has samples in the wave's unit
-  uint32_t px = 0, py = 0, sample = 0, sample_end = 0, slot = 0;
-  uint32_t gate = 0, unit_end = 0;  // wave-uniform: lanes run samples < gate; the unit ends at unit_end
-  uint32_t cur_lt = 0xffffffffu, iters = 0;  // wave-uniform: the unit's tile, loop iterations spent on it
+  uint32_t sample = 0;
+  // wave-uniform unit state (SGPRs): lanes run samples < gate; the unit (one
+  // chunk of one tile) ends at unit_end; its tile lt has its corner at (x0, y0)
+  uint32_t gate = 0, unit_end = 0, chunk_j = 0, x0 = 0, y0 = 0;
+  uint32_t cur_lt = 0xffffffffu, iters = 0;  // the unit's tile, loop iterations spent on it
   const uint64_t t_begin = ZRT_PROFILE ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint64_t offset = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
-  uint32_t depth_left = 0, nb = 0;
+  uint32_t depth_left = 0;  // attenuations stacked so far: max_depth - depth_left
   Rng<PRNG> rng;
   rng.init(0);
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
@@ -663,23 +837,21 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         if (lane == 0) u = atomicAdd(a.work_counter, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= a.total_work) break;  // the counter is exhausted
-        const uint32_t ord = u / a.n_groups, g = u - ord * a.n_groups;
+        const uint32_t ord = u / a.n_chunks, g = u - ord * a.n_chunks;
         const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;  // costliest tiles first
         cur_lt = lt;
         iters = 0;
         const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
-        px = (t % a.tiles_x) * 8u + ((uint32_t)lane & 7u);
-        py = (t / a.tiles_x) * 8u + ((uint32_t)lane >> 3);
-        const uint32_t chunk_j = g * a.unit_chunks;
-        sample = chunk_j * a.chunk;
-        unit_end = min(min(chunk_j + a.unit_chunks, a.n_chunks) * a.chunk, a.spp);
+        x0 = (t % a.tiles_x) * 8u;
+        y0 = (t / a.tiles_x) * 8u;
+        chunk_j = g;
+        sample = g * a.chunk;
+        unit_end = min(sample + a.chunk, a.spp);
         gate = min(sample + a.sync, unit_end);
-        active = px < a.xbound && py < a.height;  // else: finalize writes black
-        slot = chunk_j * a.n_slots + lt * 64u + (uint32_t)lane;  // partial is [chunk][pixel slot]
-        sample_end = min(sample + a.chunk, a.spp);
+        // lane p renders pixel p of the 8x8 tile; off-frame lanes stay idle (finalize writes black)
+        active = x0 + ((uint32_t)lane & 7u) < a.xbound && y0 + ((uint32_t)lane >> 3) < a.height;
         acc_r = acc_g = acc_b = 0.0f;
         in_sample = false;
-        offset = (uint64_t)py * a.width + px;
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[0] += t - t0; }
       continue;
@@ -689,6 +861,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
 
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
     if (!in_sample) {
+      const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
+      const uint64_t offset = (uint64_t)py * a.width + px;
       rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
       const float u = ((float)px + rand_float(rng) - 0.5f) / a.f_width;
       const float v = ((float)py + rand_float(rng) - 0.5f) / a.f_height;
@@ -698,7 +872,6 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       o = mk(a.org[0], a.org[1], a.org[2]);
       d = unit(sub(add(add(llc, scale(hor, u)), scale(ver, v)), o));
       depth_left = a.max_depth;
-      nb = 0;
       in_sample = true;
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[1] += t - t0; t0 = t; }
@@ -818,8 +991,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         } else {
           ++c_refl;
           if (depth_left > 1) {  // an attenuation pushed at depth 1 is never read
-            a.att[(uint64_t)nb * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
-            ++nb;
+            // every earlier scatter was at a depth > this one, so all were pushed
+            a.att[(uint64_t)(a.max_depth - depth_left) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
           }
           o = loc;
           d = nd;
@@ -833,7 +1006,9 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
       V3 col = L;
       if (sky) {
-        for (uint32_t i = nb; i-- > 0;) {
+        // a path that reached the sky traced at depth_left >= 1: all of its
+        // max_depth - depth_left scatters were pushed
+        for (uint32_t i = a.max_depth - depth_left; i-- > 0;) {
           const float4 at = a.att[(uint64_t)i * a.n_lanes + gl];
           col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
         }
@@ -842,12 +1017,9 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       acc_g += col.y;
       acc_b += col.z;
       in_sample = false;
-      if (++sample == sample_end) {  // chunk done: its sequential sum
-        a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
-        slot += a.n_slots;
-        sample_end = min(sample + a.chunk, a.spp);
-        acc_r = acc_g = acc_b = 0.0f;
-        active = sample < unit_end;
+      if (++sample == unit_end) {  // chunk done: its sequential sum; partial is [chunk][pixel slot]
+        a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
+        active = false;
       }
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
@@ -1092,7 +1264,7 @@ struct zrt_ctx {
   hipStream_t stream = nullptr;
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
-  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0;
+  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0;
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
@@ -1177,12 +1349,27 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
     const WideBvh wide = build_wide_bvh(leaves);
-    std::vector<float4> wn(wide.nodes.size());
-    std::memcpy(wn.data(), wide.nodes.data(), wn.size() * sizeof(float4));
+    const size_t nw = wide.nodes.size();
+#if ZRT_OCT && ZRT_OCT_COPIES
+    // one copy per ray octant o (bit k set: direction k negative) with axis k's
+    // min / max planes swapped, so float4 0-2 are the near planes, 3-5 the far
+    std::vector<float4> wn(8 * nw);
+    for (uint32_t o = 0; o < 8; ++o) {
+      float4* dst = wn.data() + o * nw;
+      std::memcpy(dst, wide.nodes.data(), nw * sizeof(float4));
+      for (size_t i = 0; i < nw; i += 8)
+        for (int k = 0; k < 3; ++k)
+          if (o >> k & 1u) std::swap(dst[i + k], dst[i + 3 + k]);
+    }
+#else
+    std::vector<float4> wn(nw);
+    std::memcpy(wn.data(), wide.nodes.data(), nw * sizeof(float4));
+#endif
+    c->wide_stack = wide.max_stack + (ZRT_OCT ? 3 : 0);  // + the dead entries of a branch-free push
     c->wnodes.upload(wn);
+    c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
-    c->wide_stack = wide.max_stack;
   } else {
     for (uint32_t i = 0; i < n; ++i) slot_to_prim.push_back(i);
   }
@@ -1333,8 +1520,6 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.spp = kProbeSpp;
   pa.chunk = kProbeSpp;
   pa.n_chunks = 1;
-  pa.unit_chunks = 1;
-  pa.n_groups = 1;
   pa.total_work = my_tiles;
   if (c->probe_partial.n < uint64_t(my_tiles) * 64u) c->probe_partial.alloc(uint64_t(my_tiles) * 64u);
   if (c->probe_scratch.n < uint64_t(kScratchSlots)) c->probe_scratch.alloc(kScratchSlots);
@@ -1464,9 +1649,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     uint32_t grid = uint32_t(c->cu_count) * uint32_t(per_cu);
     const uint32_t chunk = p->sample_chunk ? p->sample_chunk : ZRT_DEFAULT_SAMPLE_CHUNK;
     const uint32_t n_chunks = (p->samples_per_pixel + chunk - 1) / chunk;
-    const uint32_t unit_chunks = ZRT_UNIT_CHUNKS;
-    const uint32_t n_groups = (n_chunks + unit_chunks - 1) / unit_chunks;
-    const uint64_t work64 = uint64_t(my_tiles) * n_groups;  // units: (tile, group of chunks)
+    const uint64_t work64 = uint64_t(my_tiles) * n_chunks;  // units: (tile, chunk)
     if (uint64_t(my_tiles) * 64u * n_chunks >= (1ull << 32))
       return fail(ZRT_E_UNSUPPORTED, "more than 2^32 (pixel, chunk) work items");
     const uint32_t work = uint32_t(work64);
@@ -1516,12 +1699,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.stack_depth = stack_depth;
     a.wnodes = c->wnodes.p;
+    a.wide_stride = c->wide_stride;
     a.n_lanes = uint32_t(n_lanes);
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
     a.chunk = chunk;
     a.n_chunks = n_chunks;
-    a.unit_chunks = unit_chunks;
-    a.n_groups = n_groups;
     a.sync = ZRT_SYNC_SAMPLES;
     a.n_slots = my_tiles * 64u;
 
