@@ -230,6 +230,23 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
   }
   out.n_nodes = uint32_t(wide.size());
   out.nodes.resize(8 * wide.size());
+  // storage order: depth-first (pre-order, children in slot order), so a
+  // subtree's nodes are adjacent (A/B against the breadth-first construction
+  // order: equal on C4 / C5, +0.7 % on C3)
+  std::vector<int32_t> pos(wide.size(), -1);
+  {
+    std::vector<int32_t> todo{0};
+    int32_t next_pos = 0;
+    while (!todo.empty()) {
+      const int32_t wi = todo.back();
+      todo.pop_back();
+      pos[size_t(wi)] = next_pos++;
+      for (int k = wide[size_t(wi)].count - 1; k >= 0; --k) {
+        const int32_t c = wide[size_t(wi)].child[k];
+        if (N[c].leaf < 0) todo.push_back(wide_of[c]);
+      }
+    }
+  }
   uint32_t max_depth = 0;
   for (size_t wi = 0; wi < wide.size(); ++wi) {
     float4v q[8];
@@ -244,7 +261,7 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
           ref = leaves[size_t(N[c].leaf)].prim_a;
           ref_b = leaves[size_t(N[c].leaf)].prim_b;
         } else {
-          ref = wide_of[c];
+          ref = pos[size_t(wide_of[c])];
           ref_b = 0;
         }
       }
@@ -257,7 +274,7 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
       std::memcpy(&q[6].v[k], &ref, 4);
       std::memcpy(&q[7].v[k], &ref_b, 4);
     }
-    for (int k = 0; k < 8; ++k) out.nodes[8 * wi + k] = q[k];
+    for (int k = 0; k < 8; ++k) out.nodes[8 * size_t(pos[wi]) + k] = q[k];
     max_depth = std::max(max_depth, depth_of[wi]);
   }
   out.depth = max_depth;

@@ -588,7 +588,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
       next = (int32_t)stk[sp * stride];
     }
     if ((l0 | l1 | l2 | l3) != 0) {
-      const float4 rb = leaf_q[7];
+      const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
 #define ZRT_WIDE_LEAF(L, RB)                                                        \
   if (L != 0) {                                                                     \
     const int pb = as_int(RB);                                                      \
