@@ -113,6 +113,9 @@ constexpr int kBlock = 256;
 #ifndef ZRT_OCT
 #define ZRT_OCT 1  // wide tree stored once per ray octant (near / far planes pre-swapped)
 #endif
+#ifndef ZRT_LIST_SCALAR
+#define ZRT_LIST_SCALAR 1  // list mode reads its (wave-uniform) surfaces with scalar loads
+#endif
 #ifndef ZRT_OCT_COPIES
 #define ZRT_OCT_COPIES 1  // ZRT_OCT: the eight octant copies in HBM (0: one copy, planes selected per ray)
 #endif
@@ -258,11 +261,8 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
 // reference would (det >= 1e-6, t_min < t < t_max, u,v >= 0, u+v <= 1), with
 // equal-t ties going to the lower slot (= earlier in the reference's DFS).
 template <bool TIE>
-__device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int slot, const RayT& r,
-                                         float& best_t, int& best) {
-  const float4 p0 = prims[3 * slot + 0];
-  const float4 p1 = prims[3 * slot + 1];
-  const float4 p2 = prims[3 * slot + 2];
+__device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, const float4 p2, int slot,
+                                           const RayT& r, float& best_t, int& best) {
   const V3 n = mk(p2.y, p2.z, p2.w);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float det = -dot(d, n);
@@ -280,6 +280,12 @@ __device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int s
     best_t = t;
     best = slot;
   }
+}
+
+template <bool TIE>
+__device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int slot, const RayT& r,
+                                         float& best_t, int& best) {
+  tri_test_v<TIE>(prims[3 * slot + 0], prims[3 * slot + 1], prims[3 * slot + 2], slot, r, best_t, best);
 }
 
 // Sphere.hit (sphere.zig:31-41, 53-56): nearest root in (t_min, t_max).
@@ -787,7 +793,10 @@ constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 
 #ifndef ZRT_WAVES_PER_SIMD
-#define ZRT_WAVES_PER_SIMD 8  // binary/reference/list; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
+#define ZRT_WAVES_PER_SIMD 8  // binary/reference; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
+#endif
+#ifndef ZRT_WAVES_LIST
+#define ZRT_WAVES_LIST 6      // list mode (C2); A/B: w5 27.8, w6 30.3, w8 28.7 Gray/s
 #endif
 #ifndef ZRT_WAVES_WIDE
 #define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B (octant traversal, 96 VGPRs): w4 46.0, w5 50.6, w6 48.2 (spills) Gray/s
@@ -891,14 +900,23 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       float best_t = __builtin_inff();
       int best = -1;
       if (MODE == 0) {
+#if ZRT_LIST_SCALAR && defined(__HIP_DEVICE_COMPILE__)
+        // the list is wave-uniform: read it through the scalar cache (s_load)
+        typedef const __attribute__((address_space(4))) float4 cfloat4;
+        cfloat4* cprims = (cfloat4*)a.prims;
+        cfloat4* cshade = (cfloat4*)a.shade;
+#else
+        const float4* cprims = a.prims;
+        const float4* cshade = a.shade;
+#endif
         for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order, t_max shrinking
-          const uint32_t tag = __float_as_uint(a.shade[i].w);
+          const uint32_t tag = __float_as_uint(cshade[i].w);
           if (tag >> 31) {
             if (STATS) ++c_tri;
-            tri_test<false>(a.prims, (int)i, r, best_t, best);
+            tri_test_v<false>(cprims[3 * i], cprims[3 * i + 1], cprims[3 * i + 2], (int)i, r, best_t, best);
           } else {
             if (STATS) ++c_sph;
-            sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
+            sphere_test<false>(cprims[3 * i], (int)i, r, best_t, best);
           }
         }
       } else if (MODE == 3) {
@@ -1048,7 +1066,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
 }
 
 template <int MODE, int PRNG, bool STATS, class StackT>
-__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : ZRT_WAVES_PER_SIMD)
+__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : MODE == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
   render_loop<MODE, PRNG, STATS, StackT>(a);
 }
