@@ -294,3 +294,20 @@ def test_schedule_bit_exact(scenes, world):
     assert_bit_exact(plain, ref)
     gpu, gs = z.render(s, s.camera, p)
     assert gs["schedule_ms"] > 0 and gs["rays_processed"] == rs["rays_processed"]
+
+
+@pytest.mark.parametrize("rows", [1, 2, 4])
+def test_stack_overflow_rows_bit_exact(scenes, rows, monkeypatch):
+    """FAST traversal keeps at most ZRT_STACK_LDS_BYTES of its stack in LDS and
+    the deeper rows in global memory (deep trees such as scene 6).  Capping the
+    LDS part at a few rows (ZRT_STACK_LDS_ROWS) sends most pushes and pops of
+    the mesh scenes through the global rows: images and counters unchanged."""
+    monkeypatch.setenv("ZRT_STACK_LDS_ROWS", str(rows))
+    for idx in (2, 3):
+        s = scenes(idx)
+        p = z.RenderParams(24, 16, 4, 8)
+        ref, rs = O.render(s.view, s.camera, p)
+        gpu, gs = z.render(s, s.camera, p)
+        assert_bit_exact(gpu, ref)
+        for k in COUNTERS:
+            assert gs[k] == rs[k], k

@@ -28,6 +28,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -82,7 +83,9 @@ struct KArgs {
   uint32_t n_list, stack_depth, n_lanes;
   uint32_t chunk, n_chunks, sync;  // a work unit = one chunk of one tile
   uint32_t n_slots;  // this launch's pixel slots (tiles x 64): the stride of a chunk in partial
-  uint32_t wide_stride;  // float4s per octant copy of the wide tree (ZRT_OCT)
+  uint32_t wide_stride;  // float4s per octant copy of the wide tree
+  uint32_t lds_rows;     // FAST: stack rows in LDS; rows lds_rows.. stack_depth-1 in stack_ovf
+  void* stack_ovf;       // [row - lds_rows][lane] overflow rows of the FAST stack (StackT)
   unsigned long long seed_mix;
 };
 
@@ -107,17 +110,18 @@ __device__ __forceinline__ uint64_t prof_stamp() {
 }
 
 constexpr int kBlock = 256;
+#ifndef ZRT_STACK_LDS_BYTES
+#define ZRT_STACK_LDS_BYTES (28 * 1024)  // FAST traversal stack in LDS per block (5 blocks / CU fit)
+#endif
+constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #ifndef ZRT_PROBE_SPP
 #define ZRT_PROBE_SPP 1  // samples per pixel of the scheduling probe; A/B at N=8: 1, 2, 4, 8 give the same render launch
-#endif
-#ifndef ZRT_OCT
-#define ZRT_OCT 1  // wide tree stored once per ray octant (near / far planes pre-swapped)
 #endif
 #ifndef ZRT_LIST_SCALAR
 #define ZRT_LIST_SCALAR 1  // list mode reads its (wave-uniform) surfaces with scalar loads
 #endif
 #ifndef ZRT_OCT_COPIES
-#define ZRT_OCT_COPIES 1  // ZRT_OCT: the eight octant copies in HBM (0: one copy, planes selected per ray)
+#define ZRT_OCT_COPIES 1  // the wide tree stored once per ray octant (0: one copy, planes selected per ray)
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -446,7 +450,6 @@ __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   ra = tr;
 }
 
-#if ZRT_OCT
 // Two slots' slab distances (bound - o) * inv.  (Written as packed f32,
 // v_pk_add_f32 / v_pk_mul_f32 with the same roundings, this traversal ran
 // 1.2-1.8x slower: packed f32 issues at half the rate of single f32 here.)
@@ -502,10 +505,12 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
 // farther ones pushed, branch-free.
 template <bool STATS, class StackT>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
-                                              float& best_t, int& best, uint32_t& c_nodes, uint32_t& c_leaves,
-                                              uint32_t& c_tri, uint32_t& c_sph) {
+                                              uint32_t gl, float& best_t, int& best, uint32_t& c_nodes,
+                                              uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
+  const uint32_t rows = a.lds_rows;    // the first rows in LDS, the rest in global memory
+  StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float inf = __builtin_inff();
   const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
 #if ZRT_OCT_COPIES
@@ -580,10 +585,19 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     if (n != 0) {
       // push r_{n-1} .. r_1 (farthest first) and continue with the nearest; the
       // three stores are unconditional (entries above the new top are dead)
-      if (sp + 3 <= cap) {
-        stk[sp * stride] = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1);
-        stk[(sp + 1) * stride] = (StackT)(n == 4 ? r2 : r1);
-        stk[(sp + 2) * stride] = (StackT)r1;
+      const StackT e0 = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1), e1 = (StackT)(n == 4 ? r2 : r1);
+      const StackT e2 = (StackT)r1;
+      if (sp + 3 <= rows) {
+        stk[sp * stride] = e0;
+        stk[(sp + 1) * stride] = e1;
+        stk[(sp + 2) * stride] = e2;
+      } else if (sp + 3 <= cap) {  // deep trees: rows past the LDS part live in global memory
+        const StackT e[3] = {e0, e1, e2};
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+          if (sp + j < rows) stk[(sp + j) * stride] = e[j];
+          else ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+        }
       } else {
         atomicOr(a.error_flag, 1u);
       }
@@ -591,7 +605,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
       next = r0;
     } else if (sp != 0) {
       --sp;
-      next = (int32_t)stk[sp * stride];
+      next = sp < rows ? (int32_t)stk[sp * stride] : (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes];
     }
     if ((l0 | l1 | l2 | l3) != 0) {
       const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
@@ -613,97 +627,6 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   }
 #undef ZRT_LOAD_NODE
 }
-#else
-// FAST: near-first over the 4-wide tree (accel_build.cpp).  All four slots of
-// a node are tested against the t_max at node entry (a leaf passing with a
-// t_max >= the current one is a superset of what the reference opens, and
-// every primitive test still uses the current best with lower-slot
-// tie-breaking); leaf slots are intersected in place, inner slots are sorted
-// by entry distance, the farther ones pushed.
-template <bool STATS, class StackT>
-__device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
-                                              float& best_t, int& best, uint32_t& c_nodes, uint32_t& c_leaves,
-                                              uint32_t& c_tri, uint32_t& c_sph) {
-  const int stride = kBlock;
-  const uint32_t cap = a.stack_depth;
-  const float inf = __builtin_inff();
-  uint32_t sp = 0;
-  const float4* q = a.wnodes;  // the root wide node
-  float4 mnx = q[0], mny = q[1], mnz = q[2], mxx = q[3], mxy = q[4], mxz = q[5], ra = q[6];
-  for (;;) {
-    int r0 = as_int(ra.x), r1 = as_int(ra.y), r2 = as_int(ra.z), r3 = as_int(ra.w);
-    float k0, k1, k2, k3;
-    {
-      const float tb = best_t * 1.0000153f;
-      k0 = wide_slot(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, tb, r0 < 0);
-      k1 = wide_slot(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, tb, r1 < 0);
-      k2 = wide_slot(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, tb, r2 < 0);
-      k3 = wide_slot(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, tb, r3 < 0);
-    }
-    if (STATS) {
-      ++c_nodes;
-      c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
-    }
-    // leaf slots that pass: their primitive refs (a in r_k, b in the node's last float4)
-    const int l0 = r0 < 0 && k0 != inf ? r0 : 0, l1 = r1 < 0 && k1 != inf ? r1 : 0;
-    const int l2 = r2 < 0 && k2 != inf ? r2 : 0, l3 = r3 < 0 && k3 != inf ? r3 : 0;
-    const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
-    k0 = r0 < 0 ? inf : k0;
-    k1 = r1 < 0 ? inf : k1;
-    k2 = r2 < 0 ? inf : k2;
-    k3 = r3 < 0 ? inf : k3;
-    // sort (entry, ref) ascending: 5 compare-exchanges
-    cswap(k0, r0, k1, r1);
-    cswap(k2, r2, k3, r3);
-    cswap(k0, r0, k2, r2);
-    cswap(k1, r1, k3, r3);
-    cswap(k1, r1, k2, r2);
-    int32_t next = -1;
-    if (k0 != inf) {
-      // push the farther inner children (farthest first), continue with the nearest
-      if (k3 != inf) {
-        if (sp < cap) stk[sp * stride] = (StackT)r3;
-        ++sp;
-      }
-      if (k2 != inf) {
-        if (sp < cap) stk[sp * stride] = (StackT)r2;
-        ++sp;
-      }
-      if (k1 != inf) {
-        if (sp < cap) stk[sp * stride] = (StackT)r1;
-        ++sp;
-      }
-      if (sp > cap) {
-        atomicOr(a.error_flag, 1u);
-        sp = cap;
-      }
-      next = r0;
-    } else if (sp != 0) {
-      --sp;
-      next = (int32_t)stk[sp * stride];
-    }
-    if ((l0 | l1 | l2 | l3) != 0) {
-      const float4 rb = leaf_q[7];
-#define ZRT_WIDE_LEAF(L, RB)                                                        \
-  if (L != 0) {                                                                     \
-    const int pb = as_int(RB);                                                      \
-    prim_test<true, STATS>(a.prims, L, r, best_t, best, c_tri, c_sph);              \
-    if (pb != L) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
-  }
-      ZRT_WIDE_LEAF(l0, rb.x)
-      ZRT_WIDE_LEAF(l1, rb.y)
-      ZRT_WIDE_LEAF(l2, rb.z)
-      ZRT_WIDE_LEAF(l3, rb.w)
-#undef ZRT_WIDE_LEAF
-    }
-    if (next < 0) return;
-    // (issuing these loads before the leaves above was measured slower: the
-    // 28 extra live registers spill)
-    q = a.wnodes + 8 * next;
-    mnx = q[0]; mny = q[1]; mnz = q[2]; mxx = q[3]; mxy = q[4]; mxz = q[5]; ra = q[6];
-  }
-}
-#endif  // ZRT_OCT
 
 // ---------------------------------------------------------------------------
 // shading
@@ -920,7 +843,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
-        traverse_wide<STATS>(a, r, stk, best_t, best, c_nodes, c_leaves, c_tri, c_sph);
+        traverse_wide<STATS>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
@@ -1290,6 +1213,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint32_t> texels8;
   uint32_t texel_bytes = 0;
   zrt::DevBuf<float4> att;
+  zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
   zrt::DevBuf<float4> partial;
   zrt::DevBuf<uint32_t> rank_base;
@@ -1368,7 +1292,7 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     c->n_nodes = uint32_t(bvh.nodes.size());
     const WideBvh wide = build_wide_bvh(leaves);
     const size_t nw = wide.nodes.size();
-#if ZRT_OCT && ZRT_OCT_COPIES
+#if ZRT_OCT_COPIES
     // one copy per ray octant o (bit k set: direction k negative) with axis k's
     // min / max planes swapped, so float4 0-2 are the near planes, 3-5 the far
     std::vector<float4> wn(8 * nw);
@@ -1383,7 +1307,7 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     std::vector<float4> wn(nw);
     std::memcpy(wn.data(), wide.nodes.data(), nw * sizeof(float4));
 #endif
-    c->wide_stack = wide.max_stack + (ZRT_OCT ? 3 : 0);  // + the dead entries of a branch-free push
+    c->wide_stack = wide.max_stack + 3;  // + the dead entries of a branch-free push
     c->wnodes.upload(wn);
     c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
@@ -1659,8 +1583,16 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const bool stk16 = mode == 3 ? c->n_wide < 65536 : c->n_nodes < 65536;
     const uint32_t stack_depth = mode == 3 ? c->wide_stack : c->stack_depth;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
-    const size_t lds =
-        size_t(stack_depth) * zrt::kBlock * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
+    // FAST: at most kStackLdsBytes of LDS stack per block (deep trees keep their
+    // last rows in global memory, rarely touched) so the LDS never caps the
+    // occupancy the registers allow; the other traversals keep it all in LDS
+    const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
+    uint32_t lds_rows =
+        mode == 3 ? std::min<uint32_t>(stack_depth, uint32_t(zrt::kStackLdsBytes / (zrt::kBlock * entry)))
+                  : stack_depth;
+    if (const char* e = std::getenv("ZRT_STACK_LDS_ROWS"))  // tests: force the overflow rows into use
+      lds_rows = std::max<uint32_t>(1, std::min<uint32_t>(lds_rows, uint32_t(std::atoi(e))));
+    const size_t lds = size_t(lds_rows) * zrt::kBlock * entry;
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
@@ -1718,6 +1650,12 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.stack_depth = stack_depth;
     a.wnodes = c->wnodes.p;
     a.wide_stride = c->wide_stride;
+    a.lds_rows = lds_rows;
+    if (stack_depth > lds_rows) {
+      const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
+      if (c->stack_ovf.n < ovf_need) c->stack_ovf.alloc(ovf_need);
+      a.stack_ovf = c->stack_ovf.p;
+    }
     a.n_lanes = uint32_t(n_lanes);
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
     a.chunk = chunk;
