@@ -211,6 +211,22 @@ typedef struct zrt_stats {
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera,
                const zrt_params* params, float* out_rgb, zrt_stats* stats);
 
+/* raytrace.render (raytrace.zig:136-203) over several GPUs of one node, from one
+ * host thread: the frame's 8x8 tiles are dealt round-robin
+ * over devices[0..n_devices) (tile t -> rank t % n_devices), every GPU holds its
+ * own copy of the scene and renders its tiles concurrently, and ONE RCCL gather
+ * (ncclGather over xGMI, ncclCommInitAll communicators) collects them on
+ * devices[0], where they are assembled and copied to out_rgb.  The image is
+ * bit-identical to zrt_render's for any device list.  A device listed more
+ * than once runs several ranks (tests on one GPU); RCCL takes one rank per
+ * device, so such a list gathers with device-to-device copies instead.  RCCL
+ * (librccl.so.1) is opened on first use.  params->rank / world_size / device
+ * are ignored.  stats: counters summed over ranks, render_ms = the slowest
+ * rank's, gather_ms = gather + assemble, n_gpus = distinct devices. */
+int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera,
+                     const zrt_params* params, const uint32_t* devices,
+                     uint32_t n_devices, float* out_rgb, zrt_stats* stats);
+
 /* Restates Camera.init (camera.zig:17-35).  look_from/look_at/vup: float[3]. */
 int zrt_camera_init(const float look_from[3], const float look_at[3],
                     const float vup[3], float vfov_deg, float aspect_ratio,

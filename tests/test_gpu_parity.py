@@ -204,6 +204,35 @@ def test_tile_partition_invariance(scenes, world):
     assert_bit_exact(one, O.render(s.view, s.camera, p)[0])
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+@pytest.mark.parametrize("scene_index", [1, 2])
+def test_render_multi_bit_exact(scenes, scene_index, devices):
+    """zrt_render_multi (one process, several GPUs): [0] runs the RCCL gather
+    (ncclCommInitAll + ncclGather with one rank); a repeated device runs that
+    many ranks on one GPU (device-copy gather).  Same image and counters as
+    zrt_render, and as the oracle."""
+    s = scenes(scene_index)
+    p = z.RenderParams(40, 40, 4, 30 if scene_index == 1 else 20)
+    one, st1 = z.render(s, s.camera, p)
+    multi, stm = z.render_multi(s, s.camera, p, devices)
+    assert same_bits(one, multi).all()
+    for k in COUNTERS:
+        assert st1[k] == stm[k], k
+    assert stm["n_gpus"] == 1
+    assert_bit_exact(multi, O.render(s.view, s.camera, p)[0])
+
+
+def test_render_multi_errors(scenes):
+    s = scenes(2)
+    p = z.RenderParams(16, 16, 1, 20)
+    with pytest.raises(z.ZrtError) as e:
+        z.render_multi(s, s.camera, p, [])
+    assert e.value.code == z._ffi.ZRT_E_INVALID
+    with pytest.raises(z.ZrtError) as e:
+        z.render_multi(s, s.camera, p, [0, 4096])
+    assert e.value.code == z._ffi.ZRT_E_NODEVICE
+
+
 # ---- the bench configuration, checked through size-independent properties ----------
 
 def test_bench_config_properties(scenes):

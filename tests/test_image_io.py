@@ -97,12 +97,19 @@ def test_cli_arguments_and_no_device():
 
 
 @pytest.mark.gpu
-def test_cli_renders_oracle_image(tmp_path, scenes):
+@pytest.mark.parametrize("devices", [None, "0", "0,0,0"])
+def test_cli_renders_oracle_image(tmp_path, scenes, devices):
     """main.zig end to end: the CLI's PNG is the oracle image through
-    png_image.zig's quantization, and its summary lines carry the counters."""
+    png_image.zig's quantization, and its summary lines carry the counters.
+    ZRT_DEVICES renders through zrt_render_multi (RCCL gather for "0")."""
     from oracle import oracle_py as O
     out = str(tmp_path / "scene1.png")
-    r = subprocess.run([CLI, "40", "40", "4", "12", "1", out], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ)
+    env.pop("ZRT_DEVICES", None)
+    if devices:
+        env["ZRT_DEVICES"] = devices
+    r = subprocess.run([CLI, "40", "40", "4", "12", "1", out], capture_output=True, text=True, timeout=300,
+                       env=env)
     assert r.returncode == 0, r.stderr
     s = scenes(1)
     ref, rs = O.render(s.view, s.camera, z.RenderParams(40, 40, 4, 12))

@@ -116,6 +116,20 @@ def render(scene, camera: _ffi.Camera, params: RenderParams):
     return out, st.as_dict()
 
 
+def render_multi(scene, camera: _ffi.Camera, params: RenderParams, devices):
+    """raytrace.render over several GPUs from one process (zrt_render_multi): tiles
+    dealt round-robin over `devices`, one RCCL gather to devices[0].  A device
+    listed twice runs two ranks (gathered by device copies).  Same image as render()."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+    st = _ffi.Stats()
+    p = params.abi()
+    devs = (C.c_uint32 * len(devices))(*devices)
+    check(lib().zrt_render_multi(view, C.byref(camera), C.byref(p), devs, len(devices),
+                                 out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+    return out, st.as_dict()
+
+
 class RenderContext:
     """Device-resident scene (zrt_ctx_*): build + upload once, render many."""
 

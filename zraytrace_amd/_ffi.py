@@ -106,6 +106,8 @@ _P = C.c_void_p
 SIGNATURES = [
     ("zrt_render", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                              C.POINTER(C.c_float), C.POINTER(Stats)]),
+    ("zrt_render_multi", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+                                   C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_float), C.POINTER(Stats)]),
     ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_float), C.c_float, C.c_float,
                                   C.POINTER(Camera)]),

@@ -8,7 +8,9 @@
 // the reference's start and summary lines on stderr (raytrace.zig:143-159,
 // 191-201; the per-scanline progress lines of raytrace.zig:37-50 have no
 // counterpart: the frame is one launch) and writes the PNG (main.zig:33,
-// png_image.zig:96-148).  Assets come from $ZRT_ASSETS, else <exe dir>/../assets.
+// png_image.zig:96-148).  Assets come from $ZRT_ASSETS, else <exe dir>/../assets;
+// $ZRT_DEVICE picks the GPU, $ZRT_DEVICES="0,1,..." renders over several
+// (zrt_render_multi: tiles round-robin, one RCCL gather).
 #include <unistd.h>
 
 #include <chrono>
@@ -120,6 +122,17 @@ int main(int argc, char** argv) {
   params.seed = 42;  // DefaultPrng.init(42) in every scene
   params.world_size = 1;
   if (const char* dev = std::getenv("ZRT_DEVICE")) params.device = uint32_t(std::atoi(dev));
+  // $ZRT_DEVICES="0,1,...,7": tiles over those GPUs, one RCCL gather (zrt_render_multi)
+  std::vector<uint32_t> devices;
+  if (const char* list = std::getenv("ZRT_DEVICES")) {
+    for (const char* q = list; *q;) {
+      char* end = nullptr;
+      const unsigned long d = std::strtoul(q, &end, 10);
+      if (end == q) break;
+      devices.push_back(uint32_t(d));
+      q = *end == ',' ? end + 1 : end;
+    }
+  }
 
   std::fprintf(stderr, "Raytrace start\n");
   std::fprintf(stderr, " - Surfaces:                 %u\n", scene->n_prims);
@@ -132,7 +145,9 @@ int main(int argc, char** argv) {
   std::vector<float> image(size_t(width) * height * 3, 0.0f);
   zrt_stats stats;
   const auto t_render = std::chrono::steady_clock::now();
-  rc = zrt_render(scene, &camera, &params, image.data(), &stats);
+  rc = devices.empty() ? zrt_render(scene, &camera, &params, image.data(), &stats)
+                       : zrt_render_multi(scene, &camera, &params, devices.data(), uint32_t(devices.size()),
+                                          image.data(), &stats);
   if (rc != ZRT_OK) {
     std::fprintf(stderr, "error: %s\n", zrt_last_error());
     zrt_scene_free(data);

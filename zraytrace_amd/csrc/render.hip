@@ -21,8 +21,10 @@
 //     (conflict-free: every lane of a wave hits a distinct bank);
 //   * RNG: one Xoroshiro128+ (or Xoshiro256++) stream per (pixel, sample),
 //     seeded through SplitMix64 exactly as DefaultPrng.init seeds.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -31,6 +33,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -574,6 +577,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     }
     const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
     const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
+    int32_t next = -1;
     // inner slots that pass, keyed by entry distance
     float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
     float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
@@ -584,7 +588,6 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     cswap(k0, r0, k2, r2);
     cswap(k1, r1, k3, r3);
     cswap(k1, r1, k2, r2);
-    int32_t next = -1;
     if (n != 0) {
       // push r_{n-1} .. r_1 (farthest first) and continue with the nearest; the
       // three stores are unconditional (entries above the new top are dead)
@@ -1522,6 +1525,52 @@ int hip_fail(const HipError& e) {
   return fail(ZRT_E_HIP, e.where + ": " + hipGetErrorString(e.err));
 }
 
+// RCCL for zrt_render_multi, opened on first use so that single-GPU callers do
+// not load it: the copy already in the process when torch brought one (same
+// soname, librccl.so.1), else ROCm's.
+struct Rccl {
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGather) gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(h, "ncclGather"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+  });
+  if (!r.comm_init_all || !r.comm_destroy || !r.gather || !r.group_start || !r.group_end || !r.error_string)
+    throw Error(ZRT_E_UNSUPPORTED, "RCCL (librccl.so.1 with ncclGather) is not available");
+  return r;
+}
+
+#define NCCLCHK(R, expr)                                                                     \
+  do {                                                                                       \
+    const ncclResult_t r_ = (expr);                                                          \
+    if (r_ != ncclSuccess) throw ::zrt::Error(ZRT_E_HIP, std::string("RCCL ") + #expr + ": " + (R).error_string(r_)); \
+  } while (0)
+
+// ncclCommInitAll communicators, one per device, destroyed with the call.
+struct Comms {
+  const Rccl* R = nullptr;
+  std::vector<ncclComm_t> c;
+  ~Comms() {
+    for (ncclComm_t x : c)
+      if (x) (void)R->comm_destroy(x);
+  }
+};
+
 }  // namespace
 }  // namespace zrt
 
@@ -1894,6 +1943,134 @@ int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_param
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
+  }
+}
+
+int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
+                     const uint32_t* devices, uint32_t n_devices, float* out_rgb, zrt_stats* stats) {
+  if (!camera || !out_rgb || !devices) return fail(ZRT_E_INVALID, "null argument");
+  if (n_devices == 0 || n_devices > 1024) return fail(ZRT_E_INVALID, "n_devices must be in 1..1024");
+  int rc = zrt::validate_params(params);
+  if (rc) return rc;
+  for (uint32_t r = 0; r < n_devices; ++r) {
+    rc = zrt::check_device(int(devices[r]));
+    if (rc) return rc;
+  }
+  std::vector<uint32_t> distinct(devices, devices + n_devices);
+  std::sort(distinct.begin(), distinct.end());
+  distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+  const bool one_rank_per_device = distinct.size() == n_devices;
+  using CtxPtr = std::unique_ptr<zrt_ctx, int (*)(zrt_ctx*)>;
+  std::vector<CtxPtr> ctx;
+  std::vector<zrt_params> rp(n_devices, *params);
+  try {
+    const zrt::Geometry g = zrt::geometry(params);
+    std::vector<uint32_t> count(n_devices), base(n_devices + 1, 0);
+    uint32_t max_tiles = 0;
+    for (uint32_t r = 0; r < n_devices; ++r) {
+      rp[r].rank = r;
+      rp[r].world_size = n_devices;
+      rp[r].device = devices[r];
+      count[r] = zrt::rank_tiles(g, r, n_devices);
+      base[r + 1] = base[r] + count[r];
+      max_tiles = std::max(max_tiles, count[r]);
+    }
+    const size_t slot = 64 * 3;  // floats per tile
+    // every GPU: its scene copy (BVH built once per rank, as zrt_render does) and
+    // a tile buffer padded to the largest rank's (ncclGather sends equal counts)
+    std::vector<zrt::DevBuf<float>> send(n_devices);
+    for (uint32_t r = 0; r < n_devices; ++r) {
+      zrt_ctx* c = nullptr;
+      rc = zrt_ctx_create(scene, &rp[r], &c);
+      if (rc) return rc;
+      ctx.emplace_back(c, zrt_ctx_destroy);
+      HIPCHK(hipSetDevice(c->device));
+      send[r].alloc(std::max<size_t>(1, max_tiles * slot));
+    }
+    // the sampling loops, all enqueued before any is waited on
+    for (uint32_t r = 0; r < n_devices; ++r) {
+      rc = zrt_ctx_render_tiles(ctx[r].get(), camera, &rp[r], send[r].p, nullptr);
+      if (rc) return rc;
+    }
+    zrt_stats sum;
+    std::memset(&sum, 0, sizeof(sum));
+    for (uint32_t r = 0; r < n_devices; ++r) {
+      zrt_stats s;
+      rc = zrt_ctx_stats(ctx[r].get(), &s);  // waits for rank r's stream
+      if (rc) return rc;
+      if (r == 0) sum = s;
+      else {
+        sum.recursion_depth_hits += s.recursion_depth_hits;
+        sum.reflections += s.reflections;
+        sum.background_hits += s.background_hits;
+        sum.pixels_processed += s.pixels_processed;
+        sum.samples_processed += s.samples_processed;
+        sum.rays_processed += s.rays_processed;
+        sum.node_visits += s.node_visits;
+        sum.prim_tests += s.prim_tests;
+        sum.sphere_tests += s.sphere_tests;
+        sum.shade_fetches += s.shade_fetches;
+        sum.texel_fetches += s.texel_fetches;
+        sum.leaf_visits += s.leaf_visits;
+        sum.preprocess_ms = std::max(sum.preprocess_ms, s.preprocess_ms);
+        sum.upload_ms = std::max(sum.upload_ms, s.upload_ms);
+        sum.render_ms = std::max(sum.render_ms, s.render_ms);
+        sum.schedule_ms = std::max(sum.schedule_ms, s.schedule_ms);
+      }
+    }
+    // the gather to devices[0], then the rank-major un-padded order zrt_ctx_assemble reads
+    const double t0 = zrt::now_ms();
+    zrt_ctx* root = ctx[0].get();
+    HIPCHK(hipSetDevice(root->device));
+    zrt::DevBuf<float> gathered, packed, frame;
+    packed.alloc(std::max<size_t>(1, size_t(base[n_devices]) * slot));
+    frame.alloc(size_t(params->width) * params->height * 3);
+    if (one_rank_per_device) {
+      const zrt::Rccl& R = zrt::rccl();
+      gathered.alloc(std::max<size_t>(1, size_t(n_devices) * max_tiles * slot));
+      zrt::Comms comms;
+      comms.R = &R;
+      comms.c.assign(n_devices, nullptr);
+      std::vector<int> devs(devices, devices + n_devices);
+      NCCLCHK(R, R.comm_init_all(comms.c.data(), int(n_devices), devs.data()));
+      NCCLCHK(R, R.group_start());
+      for (uint32_t r = 0; r < n_devices; ++r)
+        NCCLCHK(R, R.gather(send[r].p, r == 0 ? gathered.p : nullptr, size_t(max_tiles) * slot, ncclFloat32, 0,
+                            comms.c[r], ctx[r]->stream));
+      NCCLCHK(R, R.group_end());
+      HIPCHK(hipSetDevice(root->device));
+      for (uint32_t r = 0; r < n_devices; ++r)
+        if (count[r])
+          HIPCHK(hipMemcpyAsync(packed.p + size_t(base[r]) * slot, gathered.p + size_t(r) * max_tiles * slot,
+                                size_t(count[r]) * slot * sizeof(float), hipMemcpyDeviceToDevice, root->stream));
+      // every rank's gather must be done before the communicators and the send
+      // buffers go
+      for (uint32_t r = 0; r < n_devices; ++r) {
+        HIPCHK(hipSetDevice(ctx[r]->device));
+        HIPCHK(hipStreamSynchronize(ctx[r]->stream));
+      }
+      HIPCHK(hipSetDevice(root->device));
+    } else {
+      for (uint32_t r = 0; r < n_devices; ++r)
+        if (count[r])
+          HIPCHK(hipMemcpyPeerAsync(packed.p + size_t(base[r]) * slot, root->device, send[r].p, ctx[r]->device,
+                                    size_t(count[r]) * slot * sizeof(float), root->stream));
+    }
+    rc = zrt_ctx_assemble(root, &rp[0], packed.p, frame.p, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(root->stream));
+    sum.gather_ms = zrt::now_ms() - t0;
+    HIPCHK(hipMemcpy(out_rgb, frame.p, sizeof(float) * 3 * size_t(params->width) * params->height,
+                     hipMemcpyDeviceToHost));
+    sum.n_gpus = uint32_t(distinct.size());
+    if (stats) *stats = sum;
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  } catch (const zrt::Error& e) {
+    return fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(ZRT_E_NOMEM, "OutOfMemory");
   }
 }
 
