@@ -319,6 +319,11 @@ void zrt_free(void* p);
  *      u8(std.math.clamp(255.999 * c, 0, 255)) per channel.
  * PPM: ppm_image.zig - plain P3 text, u32(c * 255.999) clamped to [0, 255].
  * Unopenable path -> ZRT_E_IO (PngError.FailedToOpenFile). */
+/* png_image.readFile (png_image.zig:19-94): an 8-bit RGB or RGBA PNG (other
+ * color types and depths: ZRT_E_UNSUPPORTED, the reference's
+ * UnsupportedPngFeature) as width*height RGB f32, row 0 = bottom, c/255, alpha
+ * dropped.  Also reads 8-bit binary PPM (P6).  *out_pixels: free with zrt_free. */
+int zrt_image_read_png(const char* path, uint32_t* width, uint32_t* height, float** out_pixels);
 int zrt_image_write_png(const char* path, const float* rgb, uint32_t width, uint32_t height);
 int zrt_image_write_ppm(const char* path, const float* rgb, uint32_t width, uint32_t height);
 

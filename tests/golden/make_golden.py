@@ -109,7 +109,7 @@ def main():
                      "t_max": 100000.0, "cases": [{"direction": [-1, 0, 0], "hit": False},
                                                   {"direction": [1, 0, 0], "hit": True}]}
     # texture.zig:90-103 (earthmap, Texture.initImageOpts(image, 0, 0); exact)
-    R["texture_earthmap"] = {"file": "assets/earthmap.ppm", "u_offset": 0.0, "v_offset": 0.0, "cases": [
+    R["texture_earthmap"] = {"file": "assets/earthmap.png", "u_offset": 0.0, "v_offset": 0.0, "cases": [
         {"uv": [0.0, 0.0], "expected": [9.21568632e-01, 9.37254905e-01, 9.49019610e-01]},
         {"uv": [0.1, 0.1], "expected": [9.25490200e-01, 9.45098042e-01, 9.56862747e-01]},
         {"uv": [0.5, 0.5], "expected": [0.0, 7.84313771e-03, 2.07843139e-01]},

@@ -1,5 +1,6 @@
 """The caller-side image writers (png_image.zig:96-148, ppm_image.zig) and the
-command line (main.zig) over the C ABI.  CPU-only except the marked test."""
+command line (main.zig) over the C ABI, and the PNG reader (png_image.zig:19-94).
+CPU-only except the marked test."""
 import os
 import struct
 import subprocess
@@ -74,6 +75,108 @@ def test_ppm_matches_reference_format(tmp_path):
     want = ppm_quantize(img)
     for y, row in enumerate(rows):
         assert row == "".join(f"{r:>3} {g:>3} {b:>3}  " for r, g, b in want[y])
+
+
+# ---- png_image.readFile (png_image.zig:19-94): zrt_image_read_png ------------------
+
+ADAM7 = ((0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2))
+
+
+def _filter_row(row, prev, bpp, ftype):
+    """PNG spec §9 filters applied to one scanline (uint8 arrays)."""
+    r = row.astype(np.int32)
+    p = prev.astype(np.int32) if prev is not None else np.zeros_like(r)
+    a = np.concatenate([np.zeros(bpp, np.int32), r[:-bpp]])
+    c = np.concatenate([np.zeros(bpp, np.int32), p[:-bpp]])
+    if ftype == 0:
+        out = r
+    elif ftype == 1:
+        out = r - a
+    elif ftype == 2:
+        out = r - p
+    elif ftype == 3:
+        out = r - (a + p) // 2
+    else:
+        est = a + p - c
+        pa, pb, pc = np.abs(est - a), np.abs(est - p), np.abs(est - c)
+        out = r - np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, p, c))
+    return (out & 0xFF).astype(np.uint8)
+
+
+def encode_test_png(pixels, interlace=False, color_type=None, depth=8, rng=None):
+    """A PNG of `pixels` (uint8 [h, w, 3 or 4], top row first) with a random
+    filter type per scanline, optionally Adam7-interlaced."""
+    h, w, ch = pixels.shape
+    bpp = ch
+    color_type = color_type if color_type is not None else (6 if ch == 4 else 2)
+    passes = ADAM7 if interlace else ((0, 0, 1, 1),)
+    raw = bytearray()
+    for x0, y0, dx, dy in passes:
+        sub = pixels[y0::dy, x0::dx]
+        if sub.shape[0] == 0 or sub.shape[1] == 0:
+            continue
+        prev = None
+        for row in sub.reshape(sub.shape[0], -1):
+            ft = int(rng.integers(0, 5))
+            raw.append(ft)
+            raw += _filter_row(row, prev, bpp, ft).tobytes()
+            prev = row
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, color_type, 0, 0, 1 if interlace else 0)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"tEXt", b"Comment\x00test")
+            + chunk(b"IDAT", zlib.compress(bytes(raw))) + chunk(b"IEND", b""))
+
+
+@pytest.mark.parametrize("interlace", [False, True], ids=["progressive", "adam7"])
+@pytest.mark.parametrize("channels", [3, 4], ids=["rgb", "rgba"])
+def test_png_reader_filters(tmp_path, interlace, channels):
+    """Every filter type, both color types png_image.zig:44 accepts, Adam7 and
+    sizes smaller than an interlace block: rows flipped, c / 255 (png_image.zig:86-87)."""
+    rng = np.random.default_rng(11 + channels)
+    for h, w in ((1, 1), (5, 7), (17, 33), (64, 9)):
+        px = rng.integers(0, 256, (h, w, channels), dtype=np.uint8)
+        p = tmp_path / f"t{h}x{w}.png"
+        p.write_bytes(encode_test_png(px, interlace=interlace, rng=rng))
+        got = z.read_png(str(p))
+        want = (px[::-1, :, :3].astype(np.float32) / np.float32(255.0)).astype(np.float32)
+        assert got.shape == (h, w, 3)
+        assert (got.view(np.uint32) == want.view(np.uint32)).all(), (h, w)
+
+
+def test_png_reader_rejects(tmp_path):
+    """png_image.zig:44-51: UnsupportedPngFeature for grey / palette / 16-bit;
+    a missing file or a damaged stream is an I/O error."""
+    rng = np.random.default_rng(5)
+    grey = tmp_path / "grey.png"
+    grey.write_bytes(encode_test_png(rng.integers(0, 256, (4, 4, 1), dtype=np.uint8), color_type=0, rng=rng))
+    deep = tmp_path / "deep.png"
+    deep.write_bytes(encode_test_png(rng.integers(0, 256, (4, 4, 6), dtype=np.uint8), color_type=2, depth=16,
+                                     rng=rng))
+    for p in (grey, deep):
+        with pytest.raises(z.ZrtError) as e:
+            z.read_png(str(p))
+        assert e.value.code == _ffi.ZRT_E_UNSUPPORTED
+    good = encode_test_png(rng.integers(0, 256, (4, 4, 3), dtype=np.uint8), rng=rng)
+    bad = bytearray(good)
+    bad[-20] ^= 0xFF  # inside IDAT: its CRC no longer matches
+    (tmp_path / "bad.png").write_bytes(bytes(bad))
+    for p in (tmp_path / "bad.png", tmp_path / "missing.png"):
+        with pytest.raises(z.ZrtError) as e:
+            z.read_png(str(p))
+        assert e.value.code == _ffi.ZRT_E_IO
+
+
+def test_reference_pngs_decode():
+    """The reference's own textures (models/images) and showcase render, as
+    copied into assets/: sizes and the README showcase's channel means."""
+    assert z.read_png(os.path.join(REPO, "assets", "earthmap.png")).shape == (512, 1024, 3)
+    assert z.read_png(os.path.join(REPO, "assets", "nitor-logo-25.png")).shape == (439, 1000, 3)  # RGBA
+    show = z.read_png(os.path.join(REPO, "assets", "showcase-7-spheres.png"))
+    assert show.shape == (1000, 1000, 3)
+    means = np.rint(show.astype(np.float64) * 255.0).reshape(-1, 3).mean(axis=0)
+    np.testing.assert_allclose(means, [102.455496, 177.713237, 149.453943], atol=1e-5)
 
 
 def test_writer_errors(tmp_path):

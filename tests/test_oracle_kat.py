@@ -111,20 +111,12 @@ def test_aabb_axes_tested_independently():
     assert O.aabb_hit([1, 1, -1], [2, 2, 1], [0, 0, 0], [1, 0.2, 0], 0.001, np.inf)
 
 
-def _read_ppm(path):
-    with open(path, "rb") as f:
-        data = f.read()
-    parts = data.split(maxsplit=4)
-    w, h = int(parts[1]), int(parts[2])
-    raw = np.frombuffer(parts[4][: w * h * 3], dtype=np.uint8).reshape(h, w, 3)
-    return raw
-
-
 def test_texture_earthmap(golden):
-    """texture.zig:90-103: PNG decode + row flip + c/255 + nearest texel (exact)."""
+    """texture.zig:90-103: PNG decode (libzrt's png_image.readFile restatement)
+    + row flip + c/255 + nearest texel (exact)."""
+    import zraytrace_amd as z
     g = golden["reference_tests"]["texture_earthmap"]
-    raw = _read_ppm(os.path.join(REPO, g["file"]))
-    img = (raw[::-1].astype(np.float32) / np.float32(255.0)).astype(np.float32)  # png_image.zig:86
+    img = z.read_png(os.path.join(REPO, g["file"]))
     for case in g["cases"]:
         got = O.texture_albedo(img, g["u_offset"], g["v_offset"], *case["uv"])
         np.testing.assert_array_equal(got, np.array(case["expected"], np.float32))

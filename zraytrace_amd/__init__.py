@@ -238,6 +238,16 @@ def debug_rng(prng: int, key: int, n: int, device: int = 0):
     return out
 
 
+def read_png(path: str):
+    """png_image.readFile (zrt_image_read_png): float32[height, width, 3], row 0 = bottom, c/255."""
+    w, h, px = C.c_uint32(), C.c_uint32(), C.POINTER(C.c_float)()
+    check(lib().zrt_image_read_png(path.encode(), C.byref(w), C.byref(h), C.byref(px)))
+    try:
+        return np.ctypeslib.as_array(px, shape=(h.value, w.value, 3)).copy()
+    finally:
+        lib().zrt_free(px)
+
+
 def write_png(path: str, image) -> None:
     """png_image.writeFile (png_image.zig:96-148) for a framebuffer[H, W, 3] (row 0 = bottom)."""
     img = np.ascontiguousarray(image, dtype=np.float32)

@@ -131,6 +131,8 @@ SIGNATURES = [
     ("zrt_obj_read", C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.POINTER(Prim)),
                                C.POINTER(C.c_uint32)]),
     ("zrt_free", None, [_P]),
+    ("zrt_image_read_png", C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                     C.POINTER(C.POINTER(C.c_float))]),
     ("zrt_image_write_png", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
     ("zrt_image_write_ppm", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
     ("zrt_bvh_build", C.c_int, [C.POINTER(Scene), C.POINTER(C.POINTER(BvhNode)),

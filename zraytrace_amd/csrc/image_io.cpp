@@ -1,5 +1,6 @@
-// image_io.cpp — the reference's image writers over the C ABI.
+// image_io.cpp — the reference's image reader and writers over the C ABI.
 //
+// png_image.zig:19-94 (readFile): decode_png below, zlib instead of libpng.
 // png_image.zig:96-148 (writeFile): 8-bit RGB, rows written top first (the
 // framebuffer's row 0 is the bottom: image_offset = (height - y - 1) * width + x),
 // each channel @floatToInt(u8, std.math.clamp(255.999 * c, 0, 0xff)).
@@ -12,7 +13,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -102,6 +105,138 @@ std::vector<uint8_t> encode_png(const float* rgb, uint32_t width, uint32_t heigh
   return out;
 }
 
+namespace {
+
+uint32_t be32(const uint8_t* p) { return uint32_t(p[0]) << 24 | uint32_t(p[1]) << 16 | uint32_t(p[2]) << 8 | p[3]; }
+
+// PNG filter types 0-4 (PNG spec §9) undone in place on one scanline.
+void unfilter_row(uint8_t* row, const uint8_t* prev, size_t n, unsigned bpp, uint8_t type) {
+  switch (type) {
+    case 0: return;
+    case 1:
+      for (size_t i = bpp; i < n; ++i) row[i] = uint8_t(row[i] + row[i - bpp]);
+      return;
+    case 2:
+      if (prev)
+        for (size_t i = 0; i < n; ++i) row[i] = uint8_t(row[i] + prev[i]);
+      return;
+    case 3:
+      for (size_t i = 0; i < n; ++i) {
+        const unsigned a = i >= bpp ? row[i - bpp] : 0, b = prev ? prev[i] : 0;
+        row[i] = uint8_t(row[i] + ((a + b) >> 1));
+      }
+      return;
+    case 4:
+      for (size_t i = 0; i < n; ++i) {
+        const int a = i >= bpp ? row[i - bpp] : 0, b = prev ? prev[i] : 0;
+        const int c = (i >= bpp && prev) ? prev[i - bpp] : 0;
+        const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+        row[i] = uint8_t(row[i] + (pa <= pb && pa <= pc ? a : pb <= pc ? b : c));
+      }
+      return;
+    default: throw Error(ZRT_E_IO, "BadPngFile: unknown filter type");
+  }
+}
+
+}  // namespace
+
+// png_image.readFile (png_image.zig:19-94) without libpng: 8-bit RGB or RGBA
+// only (other color types / depths are the reference's UnsupportedPngFeature),
+// Adam7 de-interlaced as png_read_image does, alpha dropped (png_set_filler),
+// rows flipped and each sample stored as f32 sample / 255 (png_image.zig:86-87).
+std::unique_ptr<Image> decode_png(const std::string& path, const std::vector<uint8_t>& f) {
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) throw Error(ZRT_E_IO, path + ": BadPngFile (signature)");
+  uint32_t w = 0, h = 0;
+  uint8_t depth = 0, ctype = 0, interlace = 0;
+  bool have_ihdr = false, have_iend = false;
+  std::vector<uint8_t> idat;
+  for (size_t pos = 8; pos + 12 <= f.size();) {
+    const uint32_t n = be32(&f[pos]);
+    if (n > f.size() - pos - 12) throw Error(ZRT_E_IO, path + ": BadPngFile (truncated chunk)");
+    const uint8_t* type = &f[pos + 4];
+    const uint8_t* data = &f[pos + 8];
+    if (uint32_t(crc32(0L, type, uInt(n + 4))) != be32(data + n))
+      throw Error(ZRT_E_IO, path + ": BadPngFile (chunk CRC)");
+    if (std::memcmp(type, "IHDR", 4) == 0) {
+      if (n != 13) throw Error(ZRT_E_IO, path + ": BadPngFile (IHDR)");
+      w = be32(data);
+      h = be32(data + 4);
+      depth = data[8];
+      ctype = data[9];
+      if (data[10] != 0 || data[11] != 0 || data[12] > 1) throw Error(ZRT_E_IO, path + ": BadPngFile (IHDR methods)");
+      interlace = data[12];
+      have_ihdr = true;
+    } else if (std::memcmp(type, "IDAT", 4) == 0) {
+      idat.insert(idat.end(), data, data + n);
+    } else if (std::memcmp(type, "IEND", 4) == 0) {
+      have_iend = true;
+      break;
+    }
+    pos += size_t(n) + 12;
+  }
+  if (!have_ihdr || !have_iend || w == 0 || h == 0) throw Error(ZRT_E_IO, path + ": BadPngFile");
+  // png_image.zig:44-51
+  if (ctype != 2 && ctype != 6)
+    throw Error(ZRT_E_UNSUPPORTED, path + ": UnsupportedPngFeature (color type " + std::to_string(ctype) + ")");
+  if (depth != 8)
+    throw Error(ZRT_E_UNSUPPORTED, path + ": UnsupportedPngFeature (bit depth " + std::to_string(depth) + ")");
+  if (uint64_t(w) * h > (1ull << 30)) throw Error(ZRT_E_UNSUPPORTED, path + ": image too large");
+  const unsigned bpp = ctype == 6 ? 4 : 3;
+  // Adam7 passes {x0, y0, dx, dy}; a non-interlaced image is one pass
+  static const uint32_t adam7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                       {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+  static const uint32_t single[1][4] = {{0, 0, 1, 1}};
+  const int n_pass = interlace ? 7 : 1;
+  const uint32_t(*passes)[4] = interlace ? adam7 : single;
+  size_t raw_size = 0;
+  for (int p = 0; p < n_pass; ++p) {
+    const uint32_t x0 = passes[p][0], y0 = passes[p][1], dx = passes[p][2], dy = passes[p][3];
+    if (w <= x0 || h <= y0) continue;  // an empty pass has no scanlines, not even filter bytes
+    const size_t pw = (w - x0 + dx - 1) / dx, ph = (h - y0 + dy - 1) / dy;
+    raw_size += ph * (1 + pw * bpp);
+  }
+  std::vector<uint8_t> raw(raw_size + 1);  // + 1: a stream longer than the image is an error
+  z_stream zs;
+  std::memset(&zs, 0, sizeof(zs));
+  if (inflateInit(&zs) != Z_OK) throw Error(ZRT_E_NOMEM, "OutOfMemory (inflate)");
+  zs.next_in = idat.data();
+  zs.avail_in = uInt(idat.size());
+  zs.next_out = raw.data();
+  zs.avail_out = uInt(raw.size());
+  const int zrc = inflate(&zs, Z_FINISH);
+  const size_t produced = raw.size() - zs.avail_out;
+  inflateEnd(&zs);
+  if (zrc != Z_STREAM_END || produced != raw_size) throw Error(ZRT_E_IO, path + ": BadPngFile (IDAT stream)");
+  std::vector<uint8_t> px(size_t(w) * h * bpp);
+  size_t at = 0;
+  for (int p = 0; p < n_pass; ++p) {
+    const uint32_t x0 = passes[p][0], y0 = passes[p][1], dx = passes[p][2], dy = passes[p][3];
+    if (w <= x0 || h <= y0) continue;
+    const size_t pw = (w - x0 + dx - 1) / dx, ph = (h - y0 + dy - 1) / dy, stride = pw * bpp;
+    const uint8_t* prev = nullptr;  // the first scanline of a pass has none
+    for (size_t r = 0; r < ph; ++r) {
+      uint8_t* row = &raw[at + 1];
+      unfilter_row(row, prev, stride, bpp, raw[at]);
+      for (size_t i = 0; i < pw; ++i)
+        std::memcpy(&px[((y0 + r * dy) * size_t(w) + x0 + i * dx) * bpp], row + i * bpp, bpp);
+      prev = row;
+      at += 1 + stride;
+    }
+  }
+  auto img = Image::init(w, h);
+  for (uint32_t y = 0; y < h; ++y) {
+    for (uint32_t x = 0; x < w; ++x) {
+      const uint8_t* s = &px[(size_t(y) * w + x) * bpp];
+      float* o = &img->pixels[((size_t(h) - y - 1) * w + x) * 3];  // image_offset = (height - y - 1) * width + x
+      o[0] = float(s[0]) / 255.0f;  // @intToFloat(f32, px0) / 0xff
+      o[1] = float(s[1]) / 255.0f;
+      o[2] = float(s[2]) / 255.0f;
+    }
+  }
+  return img;
+}
+
 std::string encode_ppm(const char* filename, const float* rgb, uint32_t width, uint32_t height) {
   std::string s;
   s.reserve(size_t(width) * height * 13 + 256);
@@ -131,6 +266,25 @@ int zrt_image_write_png(const char* path, const float* rgb, uint32_t width, uint
     zrt::check_image(path, rgb, width, height);
     const std::vector<uint8_t> png = zrt::encode_png(rgb, width, height);
     zrt::write_all(path, png.data(), png.size());
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return zrt::fail(ZRT_E_NOMEM, "OutOfMemory");
+  }
+}
+
+int zrt_image_read_png(const char* path, uint32_t* width, uint32_t* height, float** out_pixels) {
+  if (!path || !width || !height || !out_pixels) return zrt::fail(ZRT_E_INVALID, "null argument");
+  *out_pixels = nullptr;
+  try {
+    std::unique_ptr<zrt::Image> img = zrt::readImageFile(path);
+    float* p = static_cast<float*>(std::malloc(sizeof(float) * img->pixels.size()));
+    if (!p) return zrt::fail(ZRT_E_NOMEM, "OutOfMemory");
+    std::memcpy(p, img->pixels.data(), sizeof(float) * img->pixels.size());
+    *width = img->width;
+    *height = img->height;
+    *out_pixels = p;
     return ZRT_OK;
   } catch (const zrt::Error& e) {
     return zrt::fail(e.code, e.what());

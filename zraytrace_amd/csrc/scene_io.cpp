@@ -1,7 +1,8 @@
 // scene_io.cpp — the caller side of the seam, restated in C++:
 //   scenes.zig (scene table), obj_reader.zig (OBJ -> triangles),
-//   png_image.zig:76-89 (texture rows flipped, c/255), camera.zig:17-35,
+//   png_image.zig:19-94 (PNG textures, decoded in image_io.cpp), camera.zig:17-35,
 // plus flattening of ArrayList(Surface) into the C-ABI arrays.
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -49,20 +50,25 @@ std::unique_ptr<Image> Image::init(uint32_t width, uint32_t height) {
 }
 
 std::unique_ptr<Image> readImageFile(const std::string& path) {
-  FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) throw Error(ZRT_E_IO, "Can't open file " + path);
-  char magic[3] = {0, 0, 0};
-  unsigned w = 0, h = 0, maxv = 0;
-  if (std::fscanf(f, "%2s %u %u %u", magic, &w, &h, &maxv) != 4 || std::strcmp(magic, "P6") != 0 ||
-      maxv != 255 || w == 0 || h == 0) {
+  std::vector<uint8_t> bytes;
+  {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw Error(ZRT_E_IO, "Can't open file " + path);  // png_image.zig:32
+    unsigned char buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) bytes.insert(bytes.end(), buf, buf + n);
     std::fclose(f);
-    throw Error(ZRT_E_IO, path + ": not an 8-bit P6 image (tools/prepare_assets.py writes them)");
   }
-  std::fgetc(f);  // the single whitespace after maxval
-  std::vector<unsigned char> raw(size_t(w) * h * 3);
-  const size_t got = std::fread(raw.data(), 1, raw.size(), f);
-  std::fclose(f);
-  if (got != raw.size()) throw Error(ZRT_E_IO, path + ": truncated");
+  if (bytes.size() >= 8 && bytes[0] == 0x89 && std::memcmp(&bytes[1], "PNG", 3) == 0) return decode_png(path, bytes);
+  // binary PPM (P6, 8-bit): the same samples as a PNG, for callers that convert
+  unsigned w = 0, h = 0, maxv = 0;
+  int off = 0;
+  std::string head(bytes.begin(), bytes.begin() + std::min<size_t>(bytes.size(), 64));
+  if (std::sscanf(head.c_str(), "P6 %u %u %u%n", &w, &h, &maxv, &off) != 3 || maxv != 255 || w == 0 || h == 0)
+    throw Error(ZRT_E_IO, path + ": not a PNG or an 8-bit P6 image");
+  const size_t start = size_t(off) + 1;  // the single whitespace after maxval
+  if (bytes.size() < start + size_t(w) * h * 3) throw Error(ZRT_E_IO, path + ": truncated");
+  const unsigned char* raw = bytes.data() + start;
   auto img = Image::init(w, h);
   // png_image.zig:76-89: pixel (x, y) of the file lands at row (height - y - 1)
   for (uint32_t y = 0; y < h; ++y) {
@@ -409,8 +415,8 @@ std::unique_ptr<SceneData> buildScene(uint32_t scene_index, const std::string& a
       break;
     }
     case 1: {  // threeBalls (scenes.zig:54-100)
-      const Image* earthmap = own_image(*sd, dir + "/earthmap.ppm");
-      const Image* nitor = own_image(*sd, dir + "/nitor-logo-25.ppm");
+      const Image* earthmap = own_image(*sd, dir + "/earthmap.png");
+      const Image* nitor = own_image(*sd, dir + "/nitor-logo-25.png");
       const Material* mirror = own(*sd, Material::initMetal(Texture::initColor(Color::silver)));
       const Material* nitor_m = own(*sd, Material::initLambertian(random, Texture::initImage(nitor)));
       const Material* green_matte = own(*sd, Material::greenMatte(random));
@@ -446,7 +452,7 @@ std::unique_ptr<SceneData> buildScene(uint32_t scene_index, const std::string& a
       break;
     }
     case 4: {  // teapotAndBallCircle (scenes.zig:168-204)
-      const Image* earthmap = own_image(*sd, dir + "/earthmap.ppm");
+      const Image* earthmap = own_image(*sd, dir + "/earthmap.png");
       const Material* purple = own(*sd, Material::initLambertian(random, Texture::initImage(earthmap)));
       const float top = -2.33f, radius = 100.0f;
       const Vec3 earth_center{1.66445508e-01f, top - radius, 7.37018966e+00f};
@@ -478,8 +484,8 @@ std::unique_ptr<SceneData> buildScene(uint32_t scene_index, const std::string& a
       // det >= 1e-6 cut-off), so the BVH (1.9 M nodes, 61 MB) and the f32 textures
       // (earthmap 6.3 MB, nitor 5.3 MB) exceed every XCD's 4 MB L2.
       constexpr int kSubdiv = 4;
-      const Image* earthmap = own_image(*sd, dir + "/earthmap.ppm");
-      const Image* nitor = own_image(*sd, dir + "/nitor-logo-25.ppm");
+      const Image* earthmap = own_image(*sd, dir + "/earthmap.png");
+      const Image* nitor = own_image(*sd, dir + "/nitor-logo-25.png");
       const Material* ground = own(*sd, Material::initLambertian(random, Texture::initImage(earthmap)));
       const Material* skin = own(*sd, Material::initLambertian(random, Texture::initImage(nitor)));
       const float top = -2.33f, radius = 100.0f;

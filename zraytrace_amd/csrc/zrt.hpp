@@ -56,6 +56,8 @@ struct Image {
 // same 8-bit samples stored as P6 (tools/prepare_assets.py).  Rows are flipped
 // and scaled c/255 in f32 as png_image.zig:86 does.
 std::unique_ptr<Image> readImageFile(const std::string& path);
+// png_image.zig:19-94 on the bytes of a PNG file (image_io.cpp)
+std::unique_ptr<Image> decode_png(const std::string& path, const std::vector<uint8_t>& bytes);
 
 // DefaultPrng.init(seed): the random source render() and the materials share.
 struct DefaultPrng {
