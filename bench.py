@@ -32,6 +32,9 @@ SCENES = {0: "manAndBall: models/Man_LOD3.obj + ground sphere", 1: "threeBalls: 
           6: "texturedTeapot: the C5 substitute, 1.6 M subdivided teapot triangles + image textures"}
 # 0-5: scenes.zig:267-277; 6: DESIGN.md section 4
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (SIMD-32), 2400 MHz max clock (MI355X_MICROARCH.md: CUs, max clock, SIMD/EU rows)
+VALU_ISSUE_PEAK = 256 * 4 * 2400e6 / 2
 
 
 def log(*a):
@@ -237,7 +240,11 @@ def main():
                                  "dependent-load latency and VALU issue (DESIGN.md section 4); see valu_*.",
                          "valu_lane_util": sq.get("valu_lane_util"),
                          "valu_insts_per_ray": (round(sq["SQ_INSTS_VALU"] / max(1, st["rays_processed"]), 2)
-                                                if sq.get("SQ_INSTS_VALU") else None)},
+                                                if sq.get("SQ_INSTS_VALU") else None),
+                         # the bound this loop actually sits against: wave64 VALU instructions issued
+                         # per second over the chip's issue peak (same PMC pass and its duration)
+                         "valu_issue_frac": (round(sq["SQ_INSTS_VALU"] / (pmc["duration_ns"] * 1e-9) / VALU_ISSUE_PEAK, 4)
+                                             if sq.get("SQ_INSTS_VALU") and pmc.get("duration_ns") else None)},
             "accel": {"reference_bvh_nodes": diag["bvh_nodes"], "reference_bvh_depth": diag["bvh_max_depth"],
                       "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
