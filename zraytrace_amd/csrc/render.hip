@@ -1267,8 +1267,22 @@ struct zrt_ctx {
 namespace zrt {
 namespace {
 
+// The scene flattened for the device (host arrays, built once, uploaded to
+// every GPU that renders it).
+struct HostScene {
+  bool use_bvh = false;
+  uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0;
+  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0;
+  uint32_t texel_bytes = 0;
+  std::vector<float4> nodes, wn, prims, shade;
+  std::vector<DevMaterial> mats;
+  std::vector<float> tex, lut;
+  std::vector<uint32_t> tex8;
+  double preprocess_ms = 0;
+};
+
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
-void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
+void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
   std::vector<uint32_t> slot_to_prim;
@@ -1331,7 +1345,7 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     std::memcpy(wn.data(), wide.nodes.data(), nw * sizeof(float4));
 #endif
     c->wide_stack = wide.max_stack + 3;  // + the dead entries of a branch-free push
-    c->wnodes.upload(wn);
+    c->wn = std::move(wn);
     c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
@@ -1431,20 +1445,42 @@ void build_device_scene(zrt_ctx* c, const zrt_scene* s, bool use_bvh) {
     }
   }
   c->texel_bytes = s->n_images == 0 ? 0u : texel_count == 0 ? 4u : 12u;
-  const double t1 = now_ms();
-  c->nodes.upload(nodes);
-  c->prims.upload(prims);
-  c->shade.upload(shade);
-  c->mats.upload(mats);
-  c->texels.upload(tex);
-  c->texels8.upload(tex8);
-  c->lut255.upload(std::vector<float>(lut, lut + 256));
-  c->preprocess_ms = t1 - t0;
-  c->upload_ms = now_ms() - t1;
+  c->nodes = std::move(nodes);
+  c->prims = std::move(prims);
+  c->shade = std::move(shade);
+  c->mats = std::move(mats);
+  c->tex = std::move(tex);
+  c->tex8 = std::move(tex8);
+  c->lut.assign(lut, lut + 256);
+  c->preprocess_ms = now_ms() - t0;
   c->use_bvh = use_bvh;
   c->n_prims = n;
   c->bvh_depth = depth;
-  c->stack_depth = use_bvh ? depth + 2 : 0;
+}
+
+// Upload a flattened scene to the context's device.
+void upload_scene(zrt_ctx* c, const HostScene& h) {
+  const double t1 = now_ms();
+  c->nodes.upload(h.nodes);
+  c->wnodes.upload(h.wn);
+  c->prims.upload(h.prims);
+  c->shade.upload(h.shade);
+  c->mats.upload(h.mats);
+  c->texels.upload(h.tex);
+  c->texels8.upload(h.tex8);
+  c->lut255.upload(h.lut);
+  c->upload_ms = now_ms() - t1;
+  c->preprocess_ms = h.preprocess_ms;
+  c->use_bvh = h.use_bvh;
+  c->n_prims = h.n_prims;
+  c->n_nodes = h.n_nodes;
+  c->bvh_depth = h.bvh_depth;
+  c->stack_depth = h.use_bvh ? h.bvh_depth + 2 : 0;
+  c->n_wide = h.n_wide;
+  c->n_leaves = h.n_leaves;
+  c->wide_stack = h.wide_stack;
+  c->wide_stride = h.wide_stride;
+  c->texel_bytes = h.texel_bytes;
 }
 
 template <int MODE, int PRNG, bool STATS, class StackT>
@@ -1561,6 +1597,23 @@ const Rccl& rccl() {
     if (r_ != ncclSuccess) throw ::zrt::Error(ZRT_E_HIP, std::string("RCCL ") + #expr + ": " + (R).error_string(r_)); \
   } while (0)
 
+// A context on `device` holding an uploaded copy of a flattened scene.
+std::unique_ptr<zrt_ctx> ctx_on_device(const HostScene& h, int device) {
+  std::unique_ptr<zrt_ctx> c(new zrt_ctx);
+  c->device = device;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&c->ev_pre));
+  HIPCHK(hipEventCreate(&c->ev0));
+  HIPCHK(hipEventCreate(&c->ev1));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, c->device));
+  c->cu_count = prop.multiProcessorCount;
+  upload_scene(c.get(), h);
+  c->scratch.alloc(kScratchSlots);
+  return c;
+}
+
 // ncclCommInitAll communicators, one per device, destroyed with the call.
 struct Comms {
   const Rccl* R = nullptr;
@@ -1592,22 +1645,12 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
   if (!params) return fail(ZRT_E_INVALID, "params is null");
   rc = zrt::check_device(int(params->device));
   if (rc) return rc;
-  std::unique_ptr<zrt_ctx> c(new zrt_ctx);
   try {
-    c->device = int(params->device);
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&c->ev_pre));
-    HIPCHK(hipEventCreate(&c->ev0));
-    HIPCHK(hipEventCreate(&c->ev1));
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, c->device));
-    c->cu_count = prop.multiProcessorCount;
     // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
-    zrt::build_device_scene(c.get(), scene, use_bvh);
-    c->scratch.alloc(zrt::kScratchSlots);
-    *out = c.release();
+    zrt::HostScene h;
+    zrt::flatten_scene(&h, scene, use_bvh);
+    *out = zrt::ctx_on_device(h, int(params->device)).release();
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
@@ -1952,6 +1995,8 @@ int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt
   if (n_devices == 0 || n_devices > 1024) return fail(ZRT_E_INVALID, "n_devices must be in 1..1024");
   int rc = zrt::validate_params(params);
   if (rc) return rc;
+  rc = zrt::validate_scene(scene);
+  if (rc) return rc;
   for (uint32_t r = 0; r < n_devices; ++r) {
     rc = zrt::check_device(int(devices[r]));
     if (rc) return rc;
@@ -1976,13 +2021,15 @@ int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt
       max_tiles = std::max(max_tiles, count[r]);
     }
     const size_t slot = 64 * 3;  // floats per tile
-    // every GPU: its scene copy (BVH built once per rank, as zrt_render does) and
-    // a tile buffer padded to the largest rank's (ncclGather sends equal counts)
+    // the scene flattened once (BVH build, raytrace.zig:124-133), then every GPU
+    // gets its own copy and a tile buffer padded to the largest rank's
+    // (ncclGather sends equal counts)
+    const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
+    zrt::HostScene host;
+    zrt::flatten_scene(&host, scene, use_bvh);
     std::vector<zrt::DevBuf<float>> send(n_devices);
     for (uint32_t r = 0; r < n_devices; ++r) {
-      zrt_ctx* c = nullptr;
-      rc = zrt_ctx_create(scene, &rp[r], &c);
-      if (rc) return rc;
+      zrt_ctx* c = zrt::ctx_on_device(host, int(devices[r])).release();
       ctx.emplace_back(c, zrt_ctx_destroy);
       HIPCHK(hipSetDevice(c->device));
       send[r].alloc(std::max<size_t>(1, max_tiles * slot));
