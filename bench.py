@@ -225,6 +225,10 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_unit": "bytes per launch (rocprofv3 (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB)",
                          "traffic_source": traffic_src,
+                         # the metric's "achieved HBM GB/s": measured HBM bytes per launch over the
+                         # launch time (frac_measured against the 8 TB/s peak)
+                         "hbm_gbs_measured": (round(traffic / avg_kernel_s / 1e9, 1) if traffic else None),
+                         "frac_measured": (round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
                          "kernel": f"render_kernel (BVH {args.traversal} traversal)",
                          "algorithmic_bytes_per_launch": int(algo),
                          "per_ray": {"node_visits": round(diag["node_visits"] / max(1, diag["rays_processed"]), 2),
