@@ -201,6 +201,7 @@ typedef struct zrt_stats {
   uint32_t texel_bytes;   /* bytes per texel on the device: 4 when every image is exact 8-bit
                              (c == k/255, png_image.zig:76-89), else 12 (f32 RGB); 0: no images */
   float schedule_ms;       /* probe + sort before the render launch (included in render_ms) */
+  uint64_t order_replays;  /* FAST: rays re-traced the reference's way for an order hazard (diagnostic) */
 } zrt_stats;
 
 /* ---- entry points -------------------------------------------------------- */
@@ -226,6 +227,16 @@ int zrt_render(const zrt_scene* scene, const zrt_camera* camera,
 int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera,
                      const zrt_params* params, const uint32_t* devices,
                      uint32_t n_devices, float* out_rgb, zrt_stats* stats);
+
+/* The closest-hit query of one rayColor step (raytrace.zig:71-81: the top-level
+ * surfaces tested with t_min = 0.001 and a shrinking t_max; under BVH that is
+ * BVHNode.hit, bvh.zig:187-205) for a batch of rays on params->device, through
+ * the render loop's own traversal (params->traversal).  rays: n_rays x {origin
+ * xyz, direction xyz}, directions normalised as Ray.init does (ray.zig:11-13).
+ * out_t: the hit's t (+inf on a miss); out_prim: the index of the surface hit
+ * in scene->prims (-1 on a miss).  One-shot like zrt_render. */
+int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* rays,
+              uint32_t n_rays, float* out_t, int32_t* out_prim);
 
 /* Restates Camera.init (camera.zig:17-35).  look_from/look_at/vup: float[3]. */
 int zrt_camera_init(const float look_from[3], const float look_at[3],

@@ -790,6 +790,58 @@ static V3 random_in_unit_sphere(zs_rng* r) {
     return p;
   }
 }
+/* raytrace.zig:71-81 (the closest-hit part of rayColor) for a batch of rays */
+int oracle_trace(const zrt_scene* scene, int use_bvh, const float* rays, uint32_t n, float* out_t,
+                 int32_t* out_prim) {
+  Scene sc;
+  int rc = scene_build(&sc, scene, use_bvh);
+  if (rc) { scene_free(&sc); return rc; }
+  Diag dg = {0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    const float* q = rays + 6 * (size_t)i;
+    const Ray ray = ray_init(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]));
+    float t_max = INFINITY;
+    HitRecord closest;
+    int have = 0;
+    for (uint32_t k = 0; k < sc.n_top; ++k) {
+      HitRecord h;
+      if (surface_hit(sc.top[k], &ray, 0.001f, t_max, &h, &dg)) {
+        closest = h;
+        have = 1;
+        t_max = closest.t;
+      }
+    }
+    out_t[i] = have ? closest.t : INFINITY;
+    out_prim[i] = have ? closest.surface->index : -1;
+  }
+  scene_free(&sc);
+  return ZRT_OK;
+}
+
+/* bvh.zig:234-247 (createSurfaces) and bvh.zig:280-281 on one stream */
+void oracle_bvh_test_data(uint32_t prng, uint64_t seed, uint32_t n_spheres, uint32_t n_rays, float* spheres,
+                          float* rays) {
+  zs_rng r;
+  zs_rng_init(&r, (int)prng, seed);
+  for (uint32_t i = 0; i < n_spheres; ++i) {
+    const float x = (zs_random_float(&r) - 0.5f) * 100.0f;
+    const float y = (zs_random_float(&r) - 0.5f) * 100.0f;
+    const float z = (zs_random_float(&r) - 0.5f) * 100.0f;
+    const float radius = zs_random_float(&r) * 10.0f + 0.01f;
+    spheres[4 * (size_t)i + 0] = x;
+    spheres[4 * (size_t)i + 1] = y;
+    spheres[4 * (size_t)i + 2] = z;
+    spheres[4 * (size_t)i + 3] = radius;
+  }
+  for (uint32_t i = 0; i < n_rays; ++i) {
+    const V3 o = v_scale(random_unit_vector(&r), 100.0f);
+    const V3 d = random_unit_vector(&r);
+    float* q = rays + 6 * (size_t)i;
+    q[0] = o.x; q[1] = o.y; q[2] = o.z;
+    q[3] = d.x; q[4] = d.y; q[5] = d.z;
+  }
+}
+
 void oracle_sample_vector(uint32_t prng, uint64_t seed, int which, float out[3]) {
   zs_rng r;
   zs_rng_init(&r, (int)prng, seed);

@@ -52,6 +52,20 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera,
 int oracle_bvh_build(const zrt_scene* scene, zrt_bvh_node** nodes,
                      uint32_t* n_nodes, uint32_t* max_depth);
 
+/* One rayColor closest-hit query (raytrace.zig:71-81 over preprocessSufraces'
+ * top-level list, BVHNode.hit bvh.zig:187-205 under BVH) per ray: rays are
+ * n x {origin, direction} (Ray.init normalises), t_min 0.001.  out_t = +inf and
+ * out_prim = -1 on a miss, else the hit t and the surface's list index. */
+int oracle_trace(const zrt_scene* scene, int use_bvh, const float* rays, uint32_t n,
+                 float* out_t, int32_t* out_prim);
+
+/* The data of the reference's own BVH test (bvh.zig:234-247 createSurfaces and
+ * bvh.zig:277-282): one DefaultPrng(seed) stream draws n_spheres spheres
+ * {x, y, z, radius} and then n_rays rays {randomUnitVector * 100,
+ * randomUnitVector}. */
+void oracle_bvh_test_data(uint32_t prng, uint64_t seed, uint32_t n_spheres, uint32_t n_rays,
+                          float* spheres, float* rays);
+
 /* Camera.init (camera.zig:17-35). */
 void oracle_camera_init(const float from[3], const float at[3], const float vup[3],
                         float vfov, float aspect, zrt_camera* out);

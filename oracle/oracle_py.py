@@ -65,6 +65,9 @@ def load():
     L.oracle_texture_albedo.argtypes = [C.POINTER(_ffi.Image), C.c_float, C.c_float, C.c_float,
                                         C.c_float, f3]
     L.oracle_texture_albedo.restype = None
+    L.oracle_trace.argtypes = [S, C.c_int, f3, C.c_uint32, f3, C.POINTER(C.c_int32)]
+    L.oracle_bvh_test_data.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, f3, f3]
+    L.oracle_bvh_test_data.restype = None
     L.oracle_free.argtypes = [C.c_void_p]
     L.oracle_free.restype = None
     _lib = L
@@ -106,6 +109,32 @@ def bvh_build(scene_view):
         return nodes_to_numpy(nodes, n.value) + (depth.value,)
     finally:
         L.oracle_free(C.cast(nodes, C.c_void_p))
+
+
+def trace(scene_view, use_bvh, origins, directions):
+    """oracle_trace: closest hit per ray (t, +inf on a miss; surface list index, -1)."""
+    L = load()
+    rays = np.ascontiguousarray(np.concatenate([np.asarray(origins, np.float32).reshape(-1, 3),
+                                                np.asarray(directions, np.float32).reshape(-1, 3)], axis=1))
+    n = rays.shape[0]
+    t = np.empty(n, np.float32)
+    prim = np.empty(n, np.int32)
+    f = C.POINTER(C.c_float)
+    rc = L.oracle_trace(scene_view, int(bool(use_bvh)), rays.ctypes.data_as(f), n, t.ctypes.data_as(f),
+                        prim.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle_trace failed: {rc}")
+    return t, prim
+
+
+def bvh_test_data(prng, seed, n_spheres, n_rays):
+    """bvh.zig:234-247 + 277-282: (spheres float32[n, 4] {x, y, z, r}, rays float32[n_rays, 6])."""
+    L = load()
+    sph = np.empty((n_spheres, 4), np.float32)
+    rays = np.empty((n_rays, 6), np.float32)
+    f = C.POINTER(C.c_float)
+    L.oracle_bvh_test_data(prng, seed, n_spheres, n_rays, sph.ctypes.data_as(f), rays.ctypes.data_as(f))
+    return sph, rays
 
 
 def camera_init(look_from, look_at, vup, vfov, aspect):

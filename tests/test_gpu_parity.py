@@ -366,3 +366,98 @@ def test_c2_matches_reference_showcase_and_readme(golden, scenes):
     for key, ref in (("rays_processed", g["rays"]), ("reflections", g["reflections"]),
                      ("background_hits", g["background_hits"])):
         assert abs(st[key] - ref) <= 1e-5 * ref, (key, st[key], ref)
+
+
+# ---- the closest-hit query alone (zrt_trace): BVHNode.hit on random rays ------------
+
+def sphere_scene(spheres):
+    """ArrayList(Surface) of spheres, all with Material.black_metal (bvh.zig:244)."""
+    from zraytrace_amd import _ffi
+    import ctypes as C
+    n = len(spheres)
+    prims = (_ffi.Prim * n)()
+    for i, (x, y, zc, r) in enumerate(spheres):
+        prims[i].kind = _ffi.ZRT_PRIM_SPHERE
+        prims[i].material = 0
+        prims[i].center = _ffi.Vec3(float(x), float(y), float(zc))
+        prims[i].radius = float(r)
+    texs = (_ffi.Texture * 1)(_ffi.Texture(_ffi.ZRT_TEX_COLOR, 0, _ffi.Vec3(0, 0, 0), 0.0, 0.0))
+    mats = (_ffi.Material * 1)(_ffi.Material(_ffi.ZRT_MAT_METAL, 0, 0.0))
+    scene = _ffi.Scene(prims, n, 1, mats, texs, 1, 0, C.cast(None, C.POINTER(_ffi.Image)))
+    scene._keep = (prims, mats, texs)
+    return scene
+
+
+TRAVERSALS = [z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE, z.ZRT_TRAVERSAL_BINARY]
+
+
+def assert_same_hits(t_gpu, p_gpu, t_ref, p_ref):
+    assert (p_gpu == p_ref).all(), f"{int((p_gpu != p_ref).sum())} rays hit different surfaces"
+    assert same_bits(t_gpu, t_ref).all()
+
+
+def test_trace_reference_bvh_test():
+    """bvh.zig:262-291 restated: 3127 random spheres and 2000 random rays from one
+    DefaultPrng(42) stream; the reference asserts 10 < hits < 1500.  Here every
+    traversal, and the surface list, must return the oracle's closest hit bit
+    for bit (t_min 0.001, rayColor's, where the Zig test passes 0.0001)."""
+    sph, rays = O.bvh_test_data(z.ZRT_PRNG_XOROSHIRO128, 42, 3127, 2000)
+    scene = sphere_scene(sph)
+    t_ref, p_ref = O.trace(scene, True, rays[:, :3], rays[:, 3:])
+    hits = int((p_ref >= 0).sum())
+    assert 10 < hits < 1500, hits
+    for trav in TRAVERSALS:
+        t, p = z.trace(scene, z.RenderParams(1, 1, 1, 1, traversal=trav), rays[:, :3], rays[:, 3:])
+        assert_same_hits(t, p, t_ref, p_ref)
+    t_list, p_list = O.trace(scene, False, rays[:, :3], rays[:, 3:])
+    t, p = z.trace(scene, z.RenderParams(1, 1, 1, 1, bounded_volume_hierarchy=False), rays[:, :3], rays[:, 3:])
+    assert_same_hits(t, p, t_list, p_list)
+    # the list and the BVH agree except on exact-t ties between spheres
+    assert (p_list == p_ref).mean() > 0.999
+
+
+@pytest.mark.parametrize("scene_index,rows", [(2, None), (3, None), (0, None), (4, None), (2, "2")])
+def test_trace_mesh_rays_bit_exact(scenes, scene_index, rows, monkeypatch):
+    """Random rays inside and around the mesh scenes, plus rays aimed exactly at
+    triangle vertices and edge midpoints (ties and grazing hits): FAST, BINARY
+    and REFERENCE traversal return the oracle's surface and t for every ray.
+    rows="2": FAST with a 32-bit stack of 2 LDS rows, so both the traversal and
+    its order-hazard replay (the vertex rays have some) run on the global rows."""
+    if rows:
+        monkeypatch.setenv("ZRT_STACK_LDS_ROWS", rows)
+    from zraytrace_amd import _ffi
+    s = scenes(scene_index)
+    v = s.view.contents
+    pr = prim_array(v)
+    tri = pr[pr["kind"] == _ffi.ZRT_PRIM_TRIANGLE]
+    verts = np.concatenate([tri["a"], tri["b"], tri["c"]]).view(np.float32).reshape(-1, 3)
+    lo, hi = verts.min(0), verts.max(0)
+    rng = np.random.default_rng(scene_index)
+    n = 6000
+    o = rng.uniform(lo - (hi - lo), hi + (hi - lo), (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    k = rng.integers(0, len(tri), 3000)
+    a = tri["a"].view(np.float32).reshape(-1, 3)[k]
+    b = tri["b"].view(np.float32).reshape(-1, 3)[k]
+    c = tri["c"].view(np.float32).reshape(-1, 3)[k]
+    targets = np.concatenate([a, (a + b) * np.float32(0.5), (a + b + c) / np.float32(3.0)]).astype(np.float32)
+    o2 = np.repeat(np.asarray([s.camera.origin.x, s.camera.origin.y, s.camera.origin.z], np.float32)[None],
+                   len(targets), 0) + rng.normal(scale=0.05, size=(len(targets), 3)).astype(np.float32)
+    origins = np.concatenate([o, o2]).astype(np.float32)
+    dirs = np.concatenate([d, targets - o2]).astype(np.float32)
+    t_ref, p_ref = O.trace(s.view, True, origins, dirs)
+    assert (p_ref >= 0).mean() > 0.3
+    for trav in TRAVERSALS:
+        t, p = z.trace(s, z.RenderParams(1, 1, 1, 1, traversal=trav), origins, dirs)
+        assert_same_hits(t, p, t_ref, p_ref)
+
+
+def prim_array(v):
+    """The scene's zrt_prim array as a numpy structured array (a view)."""
+    import ctypes as C
+    from zraytrace_amd import _ffi
+    dt = np.dtype([("kind", np.uint32), ("material", np.uint32), ("center", np.float32, 3), ("radius", np.float32),
+                   ("a", np.float32, 3), ("b", np.float32, 3), ("c", np.float32, 3)])
+    assert dt.itemsize == C.sizeof(_ffi.Prim)
+    buf = (C.c_uint8 * (dt.itemsize * v.n_prims)).from_address(C.addressof(v.prims.contents))
+    return np.frombuffer(buf, dtype=dt)

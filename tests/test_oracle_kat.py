@@ -137,3 +137,23 @@ def test_math_restatements_close_to_libm():
     p = np.linspace(0, 2, 501, dtype=np.float32)
     np.testing.assert_allclose(O.math2("pow", p, np.full_like(p, 5.0)), p.astype(np.float64) ** 5, rtol=1e-6)
     assert O.math2("pow", [0.0], [5.0])[0] == 0.0 and O.math2("pow", [1.0], [5.0])[0] == 1.0
+
+
+def test_bvh_hit_reference_test():
+    """bvh.zig:262-291: 3127 random spheres, 2000 random rays from DefaultPrng(42);
+    the reference asserts 10 < hits < 1500 through BVHNode.hit.  The oracle's
+    reference-order traversal satisfies it and agrees with the plain surface list."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from test_gpu_parity import sphere_scene
+    sph, rays = O.bvh_test_data(0, 42, 3127, 2000)
+    f = O.prng_f32(0, 42, 4)  # the first sphere is the stream's first four floats
+    np.testing.assert_array_equal(sph[0], np.array([(f[0] - np.float32(0.5)) * np.float32(100),
+                                                    (f[1] - np.float32(0.5)) * np.float32(100),
+                                                    (f[2] - np.float32(0.5)) * np.float32(100),
+                                                    f[3] * np.float32(10) + np.float32(0.01)], np.float32))
+    scene = sphere_scene(sph)
+    t, p = O.trace(scene, True, rays[:, :3], rays[:, 3:])
+    assert 10 < int((p >= 0).sum()) < 1500
+    t2, p2 = O.trace(scene, False, rays[:, :3], rays[:, 3:])
+    assert (p == p2).all() and ((t == t2) | (np.isinf(t) & np.isinf(t2))).all()

@@ -130,6 +130,20 @@ def render_multi(scene, camera: _ffi.Camera, params: RenderParams, devices):
     return out, st.as_dict()
 
 
+def trace(scene, params: RenderParams, origins, directions):
+    """Closest hit of each ray (zrt_trace): (t float32[n], +inf on a miss; prim int32[n], -1 on a miss)."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    rays = np.ascontiguousarray(np.concatenate([np.asarray(origins, np.float32).reshape(-1, 3),
+                                                np.asarray(directions, np.float32).reshape(-1, 3)], axis=1))
+    n = rays.shape[0]
+    t = np.empty(n, np.float32)
+    prim = np.empty(n, np.int32)
+    p = params.abi()
+    check(lib().zrt_trace(view, C.byref(p), rays.ctypes.data_as(C.POINTER(C.c_float)), n,
+                          t.ctypes.data_as(C.POINTER(C.c_float)), prim.ctypes.data_as(C.POINTER(C.c_int32))))
+    return t, prim
+
+
 class RenderContext:
     """Device-resident scene (zrt_ctx_*): build + upload once, render many."""
 

@@ -91,7 +91,8 @@ class Stats(C.Structure):
                 ("used_bvh", C.c_uint32), ("bvh_nodes", C.c_uint32),
                 ("bvh_max_depth", C.c_uint32), ("n_gpus", C.c_uint32),
                 ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32),
-                ("texel_bytes", C.c_uint32), ("schedule_ms", C.c_float)]
+                ("texel_bytes", C.c_uint32), ("schedule_ms", C.c_float),
+                ("order_replays", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -108,6 +109,8 @@ SIGNATURES = [
                              C.POINTER(C.c_float), C.POINTER(Stats)]),
     ("zrt_render_multi", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                                    C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_float), C.POINTER(Stats)]),
+    ("zrt_trace", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_float), C.c_uint32,
+                            C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_float), C.c_float, C.c_float,
                                   C.POINTER(Camera)]),

@@ -88,13 +88,15 @@ struct KArgs {
   uint32_t n_slots;  // this launch's pixel slots (tiles x 64): the stride of a chunk in partial
   uint32_t wide_stride;  // float4s per octant copy of the wide tree
   uint32_t lds_rows;     // FAST: stack rows in LDS; rows lds_rows.. stack_depth-1 in stack_ovf
+  uint32_t ref_stack;    // rows the reference traversal needs (FAST's order-hazard replay)
+  const uint32_t* __restrict__ leaf_of_slot;  // primitive slot -> its reference BVH leaf node
   void* stack_ovf;       // [row - lds_rows][lane] overflow rows of the FAST stack (StackT)
   unsigned long long seed_mix;
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
-       kLeaves, kNumCounters };
+       kLeaves, kReplays, kNumCounters };
 constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 24;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
@@ -125,6 +127,18 @@ constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #endif
 #ifndef ZRT_OCT_COPIES
 #define ZRT_OCT_COPIES 1  // the wide tree stored once per ray octant (0: one copy, planes selected per ray)
+#endif
+#ifndef ZRT_ORDER_EXACT
+#define ZRT_ORDER_EXACT 1  // FAST / BINARY: re-trace order-hazard rays the reference's way (0: A/B only, not exact)
+#endif
+#ifndef ZRT_LEAF_LOOP
+#define ZRT_LEAF_LOOP 1  // 16-bit stack too: opened leaves walked in one loop (one copy of the primitive tests)
+#endif
+#ifndef ZRT_HAZARD_ENTRY
+#define ZRT_HAZARD_ENTRY 1  // also replay rays whose best hit lies below its own leaf's loose entry
+#endif
+#if ZRT_HAZARD_ENTRY && !ZRT_OCT_COPIES
+#error "the FAST entry test reads the near planes of the octant copies (ZRT_OCT_COPIES=1)"
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -264,12 +278,51 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   return ok;
 }
 
+__device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
+
+// Order hazards.  The reference tests each leaf against the best
+// hit of the leaves before it in its DFS order, so the hit FAST finds closest is
+// one the reference never reaches when a hit of another leaf lies between it and
+// its own leaf's loose entry (the two roundings disagree at shared vertices on a
+// box face).  TRACK flags such near ties in the sign bit of best_t (a hit's t is
+// > t_min > 0; every reader takes |best_t|, a free source modifier), so the
+// flag costs no register: set when another hit lies within kNearTie of the best.
+constexpr float kNearTie = 1.00006104f;  // 1 + 2^-14
+
+template <bool TIE, bool TRACK>
+__device__ __forceinline__ void accept_hit(float t, int slot, float& best_t, int& best, const RayT& r,
+                                           const float* leafp) {
+  if (!TRACK) {
+    const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
+    if (in_range) {
+      best_t = t;
+      best = slot;
+    }
+    return;
+  }
+  const float bt = __builtin_fabsf(best_t);
+  if (t < bt || (t == bt && slot < best)) {
+    bool near = t < bt ? bt <= t * kNearTie : best_t < 0.0f;  // an equal-t swap keeps the flag
+    if (leafp) {
+      // FAST: the leaf's loose entry E (aabb.zig:109-127; its near planes come first
+      // in the octant copy) above the hit by more than the band also flags the ray
+      const float e = __builtin_fmaxf(__builtin_fmaxf((leafp[0] - r.ox) * r.ix, (leafp[4] - r.oy) * r.iy),
+                                      __builtin_fmaxf((leafp[8] - r.oz) * r.iz, 0.001f));
+      near = near || e > t * kNearTie;
+    }
+    best_t = near ? -t : t;
+    best = slot;
+  } else if (t > bt && t <= bt * kNearTie) {
+    best_t = -bt;
+  }
+}
+
 // Triangle.hit (triangle.zig:48-70) for the candidate slot; accepts when the
 // reference would (det >= 1e-6, t_min < t < t_max, u,v >= 0, u+v <= 1), with
 // equal-t ties going to the lower slot (= earlier in the reference's DFS).
-template <bool TIE>
+template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, const float4 p2, int slot,
-                                           const RayT& r, float& best_t, int& best) {
+                                           const RayT& r, float& best_t, int& best, const float* leafp = nullptr) {
   const V3 n = mk(p2.y, p2.z, p2.w);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float det = -dot(d, n);
@@ -282,23 +335,20 @@ __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, con
   const float u = dot(e2, dao) * inv_det;
   const float v = -dot(e1, dao) * inv_det;
   const float t = dot(ao, n) * inv_det;
-  const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
-  if (t > 0.001f && in_range && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
-    best_t = t;
-    best = slot;
-  }
+  if (t > 0.001f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, leafp);
 }
 
-template <bool TIE>
+template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int slot, const RayT& r,
-                                         float& best_t, int& best) {
-  tri_test_v<TIE>(prims[3 * slot + 0], prims[3 * slot + 1], prims[3 * slot + 2], slot, r, best_t, best);
+                                         float& best_t, int& best, const float* leafp = nullptr) {
+  tri_test_v<TIE, TRACK>(prims[3 * slot + 0], prims[3 * slot + 1], prims[3 * slot + 2], slot, r, best_t, best,
+                         leafp);
 }
 
 // Sphere.hit (sphere.zig:31-41, 53-56): nearest root in (t_min, t_max).
-template <bool TIE>
+template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT& r, float& best_t,
-                                            int& best) {
+                                            int& best, const float* leafp = nullptr) {
   const V3 oc = mk(r.ox - c.x, r.oy - c.y, r.oz - c.z);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float half_b = dot(oc, d);
@@ -308,28 +358,98 @@ __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT
   const float root = dev::sqrt_rn(disc);
   const float t1 = -half_b - root;
   const float t = (t1 > 0.001f) ? t1 : (-half_b + root);
-  const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
-  if (t > 0.001f && in_range) {
-    best_t = t;
-    best = slot;
-  }
+  if (t > 0.001f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, leafp);
 }
 
-template <bool TIE, bool STATS>
+template <bool TIE, bool STATS, bool TRACK = false>
 __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int ref, const RayT& r,
-                                          float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph) {
+                                          float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph,
+                                          const float* leafp = nullptr) {
   const int code = -ref - 1;
   const int slot = code >> 1;
   if (code & 1) {
     if (STATS) ++c_tri;
-    tri_test<TIE>(prims, slot, r, best_t, best);
+    tri_test<TIE, TRACK>(prims, slot, r, best_t, best, leafp);
   } else {
     if (STATS) ++c_sph;
-    sphere_test<TIE>(prims[3 * slot], slot, r, best_t, best);
+    sphere_test<TIE, TRACK>(prims[3 * slot], slot, r, best_t, best, leafp);
   }
 }
 
-__device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
+// The reference's loose entry of a box (aabb.zig:109-127): the largest per-axis
+// max(t0, t_min) after the swap of aabb.zig:116-118, the t_max a test of the box
+// needs to exceed.
+__device__ __forceinline__ float loose_entry(const float4 lo, const float4 hi, const RayT& r) {
+  const float nx = ((r.ix < 0.0f ? hi.x : lo.x) - r.ox) * r.ix;
+  const float ny = ((r.iy < 0.0f ? hi.y : lo.y) - r.oy) * r.iy;
+  const float nz = ((r.iz < 0.0f ? hi.z : lo.z) - r.oz) * r.iz;
+  return __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, 0.001f));
+}
+
+// Order hazard of a hit found by a near-first traversal (best_t's sign cleared
+// here): a near tie was flagged (the reference may reach the other hit first and
+// then reject the best's leaf), or the loose entry E of the best's own reference
+// leaf lies above the best hit by more than the near-tie band (hits in leaves
+// culled against the best could then be below E).  Such rays are traced again
+// the reference's way.
+template <bool ENTRY>
+__device__ __forceinline__ bool order_hazard(const KArgs& a, const RayT& r, float& best_t, int best) {
+  const bool near = best_t < 0.0f;
+  best_t = __builtin_fabsf(best_t);
+  if (best < 0) return false;
+  if (near || !ENTRY) return near;  // FAST folds the entry test into the flag (accept_hit)
+#if ZRT_HAZARD_ENTRY
+  const uint32_t leaf = a.leaf_of_slot[best];  // the reference BVH node holding slot `best`
+  const float e = loose_entry(a.nodes[2 * leaf], a.nodes[2 * leaf + 1], r);
+  return e > best_t * kNearTie;
+#else
+  (void)a; (void)r;
+  return false;
+#endif
+}
+
+#ifndef ZRT_REPLAY_INLINE
+#define ZRT_REPLAY_INLINE 1
+#endif
+#if ZRT_REPLAY_INLINE
+#define ZRT_REPLAY_ATTR __forceinline__
+#else
+#define ZRT_REPLAY_ATTR __noinline__
+#endif
+template <class StackT>
+__device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, StackT* __restrict__ stk, uint32_t gl,
+                                              float& best_t, int& best) {
+  const uint32_t rows = a.lds_rows, cap = a.ref_stack;
+  StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
+  best_t = __builtin_inff();
+  best = -1;
+  uint32_t c_tri = 0, c_sph = 0;
+  stk[0] = 0;
+  uint32_t sp = 1;
+  while (sp > 0) {
+    --sp;
+    const int idx = sp < rows ? (int)stk[sp * kBlock] : (int)ovf[(size_t)(sp - rows) * a.n_lanes];
+    const float4 lo = a.nodes[2 * idx], hi = a.nodes[2 * idx + 1];
+    float e;
+    if (!box_test<false>(lo, hi, r, best_t, &e)) continue;
+    const int left = as_int(lo.w), right = as_int(hi.w);
+    if (left < 0) {
+      prim_test<false, false>(a.prims, left, r, best_t, best, c_tri, c_sph);
+      if (right != left) prim_test<false, false>(a.prims, right, r, best_t, best, c_tri, c_sph);
+    } else if (sp + 2 <= cap) {
+      const StackT v[2] = {(StackT)right, (StackT)left};
+#pragma unroll
+      for (uint32_t j = 0; j < 2; ++j) {
+        if (sp + j < rows) stk[(sp + j) * kBlock] = v[j];
+        else ovf[(size_t)(sp + j - rows) * a.n_lanes] = v[j];
+      }
+      sp += 2;
+    } else {
+      atomicOr(a.error_flag, 1u);
+    }
+  }
+}
+
 
 // Closest hit over the BVH.  FAST: near-first order with the narrowed slab
 // test; REFERENCE: left-first DFS with exactly bvh.zig:187-205's tests.
@@ -344,17 +464,17 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
-    if (!box_test<true>(lo, hi, r, best_t * 1.0000153f, &e)) return;
+    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * 1.0000153f, &e)) return;
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
-        prim_test<true, STATS>(a.prims, left, r, best_t, best, c_tri, c_sph);
-        if (right != left) prim_test<true, STATS>(a.prims, right, r, best_t, best, c_tri, c_sph);
+        prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, left, r, best_t, best, c_tri, c_sph);
+        if (right != left) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, right, r, best_t, best, c_tri, c_sph);
       } else {
         const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
         const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
         if (STATS) c_nodes += 2;
-        const float tb = best_t * 1.0000153f;
+        const float tb = __builtin_fabsf(best_t) * 1.0000153f;
         float el, er;
         const bool hl = box_test<true>(l0, l1, r, tb, &el);
         const bool hr = box_test<true>(r0, r1, r, tb, &er);
@@ -378,15 +498,18 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const int idx = sp < cap ? stk[sp * stride] : 0;
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
-        if (box_test<true>(p0, p1, r, best_t * 1.0000153f, &e)) {
+        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * 1.0000153f, &e)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
           found = true;
           break;
         }
       }
-      if (!found) return;
+      if (!found) break;
     }
+    // the order hazard of DESIGN.md §3, as in traverse_wide (the stack is all in LDS here)
+    if (ZRT_ORDER_EXACT && order_hazard<true>(a, r, best_t, best))
+      reference_replay<StackT>(a, r, stk, 0u, best_t, best);
   } else {
     stk[0] = 0;
     sp = 1;
@@ -509,7 +632,8 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
 template <bool STATS, class StackT>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                               uint32_t gl, float& best_t, int& best, uint32_t& c_nodes,
-                                              uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph) {
+                                              uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
+                                              uint32_t& c_replays) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
   // the first rows in LDS, the rest in global memory (32-bit stacks only: the
@@ -541,7 +665,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   ZRT_LOAD_NODE(q)
   for (;;) {
     int r0 = as_int(ra.x), r1 = as_int(ra.y), r2 = as_int(ra.z), r3 = as_int(ra.w);
-    const float tb = best_t * 1.0000153f;
+    const float tb = __builtin_fabsf(best_t) * 1.0000153f;
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
@@ -617,7 +741,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     // order, so lanes that opened different slots share loop trips (results
     // are order-independent: the closest t, ties to the lower slot).  A/B: C5
     // +2.9 %, C3 +2.2 % (not used: 16-bit stack), C4 -0.4 %.
-    if constexpr (sizeof(StackT) == 4) {
+    if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
       uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
       if (open != 0) {
       const float4 rb = leaf_q[7];
@@ -626,29 +750,39 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
         open &= open - 1u;
         const int L = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
         const int pb = as_int(k == 0 ? rb.x : k == 1 ? rb.y : k == 2 ? rb.z : rb.w);
-        prim_test<true, STATS>(a.prims, L, r, best_t, best, c_tri, c_sph);
-        if (pb != L) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph);
+        const float* lp = ZRT_HAZARD_ENTRY ? reinterpret_cast<const float*>(leaf_q) + k : nullptr;
+        prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);
+        if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
       } while (open != 0);
       }
     } else if ((l0 | l1 | l2 | l3) != 0) {
       const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
-#define ZRT_WIDE_LEAF(L, RB)                                                        \
-  if (L != 0) {                                                                     \
-    const int pb = as_int(RB);                                                      \
-    prim_test<true, STATS>(a.prims, L, r, best_t, best, c_tri, c_sph);              \
-    if (pb != L) prim_test<true, STATS>(a.prims, pb, r, best_t, best, c_tri, c_sph); \
+#define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
+  if (L != 0) {                                                                                     \
+    const int pb = as_int(RB);                                                                      \
+    const float* lp = ZRT_HAZARD_ENTRY ? reinterpret_cast<const float*>(leaf_q) + K : nullptr;       \
+    prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);              \
+    if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp); \
   }
-      ZRT_WIDE_LEAF(l0, rb.x)
-      ZRT_WIDE_LEAF(l1, rb.y)
-      ZRT_WIDE_LEAF(l2, rb.z)
-      ZRT_WIDE_LEAF(l3, rb.w)
+      ZRT_WIDE_LEAF(l0, rb.x, 0)
+      ZRT_WIDE_LEAF(l1, rb.y, 1)
+      ZRT_WIDE_LEAF(l2, rb.z, 2)
+      ZRT_WIDE_LEAF(l3, rb.w, 3)
 #undef ZRT_WIDE_LEAF
     }
-    if (next < 0) return;
+    if (next < 0) break;
     q = a.wnodes + (base + 8u * (uint32_t)next);
     ZRT_LOAD_NODE(q)
   }
 #undef ZRT_LOAD_NODE
+  if (ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best)) {
+    if (STATS) ++c_replays;
+#if ZRT_REPLAY_OFF
+    best_t = -best_t;  // A/B only: the replay's cost without its code (results not exact)
+#else
+    reference_replay<StackT>(a, r, stk, gl, best_t, best);
+#endif
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -770,7 +904,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   Rng<PRNG> rng;
   rng.init(0);
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
-  uint32_t c_shade = 0, c_tex = 0, c_leaves = 0;
+  uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
 
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
   for (;;) {
@@ -866,7 +1000,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
-        traverse_wide<STATS>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph);
+        traverse_wide<STATS>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
@@ -1008,6 +1142,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     wave_add_u64(&a.counters[kShades], c_shade);
     wave_add_u64(&a.counters[kTexels], c_tex);
     wave_add_u64(&a.counters[kLeaves], c_leaves);
+    wave_add_u64(&a.counters[kReplays], c_replays);
   }
 }
 
@@ -1023,6 +1158,41 @@ __global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : MODE == 0
 template <int PRNG, class StackT>
 __global__ void __launch_bounds__(kBlock, ZRT_WAVES_WIDE) schedule_probe_kernel(const KArgs a) {
   render_loop<3, PRNG, false, StackT>(a);
+}
+
+// Closest hit of a batch of rays (zrt_trace): the top-level query of rayColor
+// (raytrace.zig:71-81, t_min 0.001, t_max shrinking) through the same
+// traversal code as the render loop, one lane per ray.  Ray.init normalises the
+// direction (ray.zig:11-13).  Result: t (+inf on a miss) and the device slot.
+template <int MODE, class StackT>
+__global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const float* __restrict__ rays, uint32_t n,
+                                                       float* __restrict__ out_t, int32_t* __restrict__ out_slot) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
+  const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
+  if (gl >= n) return;
+  const float* q = rays + 6ull * gl;
+  const V3 d = unit(mk(q[3], q[4], q[5]));
+  RayT r;
+  r.ox = q[0]; r.oy = q[1]; r.oz = q[2];
+  r.dx = d.x; r.dy = d.y; r.dz = d.z;
+  r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+  float best_t = __builtin_inff();
+  int best = -1;
+  uint32_t c_nodes = 0, c_leaves = 0, c_tri = 0, c_sph = 0;
+  if (MODE == 0) {
+    for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order
+      if (__float_as_uint(a.shade[i].w) >> 31) tri_test<false>(a.prims, (int)i, r, best_t, best);
+      else sphere_test<false>(a.prims[3 * i], (int)i, r, best_t, best);
+    }
+  } else if (MODE == 3) {
+    uint32_t c_replays = 0;
+    traverse_wide<false>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
+  } else {
+    traverse_bvh<MODE == 1, false>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
+  }
+  out_t[gl] = best < 0 ? __builtin_inff() : best_t;
+  out_slot[gl] = best;
 }
 
 // Per-pixel sum of the chunk sums in chunk order, times 1/spp
@@ -1229,11 +1399,13 @@ struct zrt_ctx {
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
   uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0;
+  std::vector<uint32_t> slot_to_prim;  // device primitive slot -> reference list index
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels, lut255;
   zrt::DevBuf<uint32_t> texels8;
+  zrt::DevBuf<uint32_t> leaf_of_slot;
   uint32_t texel_bytes = 0;
   zrt::DevBuf<float4> att;
   zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
@@ -1278,6 +1450,8 @@ struct HostScene {
   std::vector<DevMaterial> mats;
   std::vector<float> tex, lut;
   std::vector<uint32_t> tex8;
+  std::vector<uint32_t> slot_to_prim;  // device primitive slot -> reference list index
+  std::vector<uint32_t> leaf_of_slot;  // device primitive slot -> its reference BVH leaf node
   double preprocess_ms = 0;
 };
 
@@ -1285,7 +1459,7 @@ struct HostScene {
 void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
-  std::vector<uint32_t> slot_to_prim;
+  std::vector<uint32_t> slot_to_prim, leaf_of_slot;
   std::vector<float4> nodes;
   uint32_t depth = 0;
   if (use_bvh) {
@@ -1309,6 +1483,11 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
       const int32_t l = ref_of(b.left);
       const int32_t r = ref_of(b.right);
       if (b.left < 0) {  // a reference leaf: its box and its primitive refs
+        for (const int32_t ref : {l, r}) {
+          const uint32_t slot = uint32_t(-ref - 1) >> 1;
+          if (leaf_of_slot.size() <= slot) leaf_of_slot.resize(slot + 1);
+          leaf_of_slot[slot] = uint32_t(i);
+        }
         RefLeaf L;
         for (int k = 0; k < 3; ++k) {
           L.mn[k] = b.mn[k];
@@ -1452,6 +1631,8 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
   c->tex = std::move(tex);
   c->tex8 = std::move(tex8);
   c->lut.assign(lut, lut + 256);
+  c->slot_to_prim = std::move(slot_to_prim);
+  c->leaf_of_slot = std::move(leaf_of_slot);
   c->preprocess_ms = now_ms() - t0;
   c->use_bvh = use_bvh;
   c->n_prims = n;
@@ -1469,6 +1650,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->texels.upload(h.tex);
   c->texels8.upload(h.tex8);
   c->lut255.upload(h.lut);
+  c->leaf_of_slot.upload(h.leaf_of_slot);
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -1481,6 +1663,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->wide_stack = h.wide_stack;
   c->wide_stride = h.wide_stride;
   c->texel_bytes = h.texel_bytes;
+  c->slot_to_prim = h.slot_to_prim;
 }
 
 template <int MODE, int PRNG, bool STATS, class StackT>
@@ -1695,10 +1878,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // FAST: a 16-bit stack when node indices fit and the whole stack fits the
     // LDS budget (else the 32-bit flavour, whose deep rows go to global memory)
     const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
-    const bool stk16 = mode == 3 ? c->n_wide < 65536 && !force_rows &&
-                                       size_t(c->wide_stack) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
+    // (FAST also holds the reference traversal's rows for its order-hazard replay)
+    const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
+    const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
+                                       size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
                                  : c->n_nodes < 65536;
-    const uint32_t stack_depth = mode == 3 ? c->wide_stack : c->stack_depth;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
     // FAST: at most kStackLdsBytes of LDS stack per block (deep trees keep their
     // last rows in global memory, rarely touched) so the LDS never caps the
@@ -1765,6 +1949,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.total_work = work;
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.stack_depth = stack_depth;
+    a.ref_stack = c->stack_depth;
+    a.leaf_of_slot = c->leaf_of_slot.p;
     a.wnodes = c->wnodes.p;
     a.wide_stride = c->wide_stride;
     a.lds_rows = lds_rows;
@@ -1845,6 +2031,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->shade_fetches = h[zrt::kShades];
     out->texel_fetches = h[zrt::kTexels];
     out->leaf_visits = h[zrt::kLeaves];
+    out->order_replays = h[zrt::kReplays];
     out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
     out->wide_nodes = c->n_wide;
     out->texel_bytes = c->texel_bytes;
@@ -2111,6 +2298,91 @@ int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt
                      hipMemcpyDeviceToHost));
     sum.n_gpus = uint32_t(distinct.size());
     if (stats) *stats = sum;
+    return ZRT_OK;
+  } catch (const zrt::HipError& e) {
+    return zrt::hip_fail(e);
+  } catch (const zrt::Error& e) {
+    return fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(ZRT_E_NOMEM, "OutOfMemory");
+  }
+}
+
+int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* rays, uint32_t n_rays, float* out_t,
+              int32_t* out_prim) {
+  if (!params || (n_rays && (!rays || !out_t || !out_prim))) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::validate_scene(scene);
+  if (rc) return rc;
+  if (params->traversal > ZRT_TRAVERSAL_BINARY) return fail(ZRT_E_INVALID, "unknown traversal");
+  rc = zrt::check_device(int(params->device));
+  if (rc) return rc;
+  if (n_rays == 0) return ZRT_OK;
+  try {
+    const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
+    zrt::HostScene h;
+    zrt::flatten_scene(&h, scene, use_bvh);
+    std::unique_ptr<zrt_ctx> c = zrt::ctx_on_device(h, int(params->device));
+    const int mode = !c->use_bvh ? 0
+                     : params->traversal == ZRT_TRAVERSAL_REFERENCE ? 2
+                     : params->traversal == ZRT_TRAVERSAL_BINARY ? 1 : 3;
+    const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
+    const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
+    const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
+                                       size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
+                                 : c->n_nodes < 65536;
+    const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
+    uint32_t lds_rows =
+        mode == 3 ? std::min<uint32_t>(stack_depth, uint32_t(zrt::kStackLdsBytes / (zrt::kBlock * entry)))
+                  : stack_depth;
+    if (mode == 3 && force_rows)
+      lds_rows = std::max<uint32_t>(1, std::min<uint32_t>(lds_rows, uint32_t(std::atoi(force_rows))));
+    const uint32_t grid = (n_rays + zrt::kBlock - 1) / zrt::kBlock;
+    const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
+    zrt::DevBuf<float> d_rays, d_t;
+    zrt::DevBuf<int32_t> d_slot;
+    d_rays.alloc(6ull * n_rays);
+    d_t.alloc(n_rays);
+    d_slot.alloc(n_rays);
+    HIPCHK(hipMemcpy(d_rays.p, rays, sizeof(float) * 6ull * n_rays, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->scratch.p, 0, zrt::kScratchSlots * sizeof(unsigned long long)));
+    zrt::KArgs a{};
+    a.nodes = c->nodes.p;
+    a.prims = c->prims.p;
+    a.shade = c->shade.p;
+    a.wnodes = c->wnodes.p;
+    a.wide_stride = c->wide_stride;
+    a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
+    a.n_list = c->use_bvh ? 0 : c->n_prims;
+    a.stack_depth = stack_depth;
+    a.ref_stack = c->stack_depth;
+    a.leaf_of_slot = c->leaf_of_slot.p;
+    a.lds_rows = lds_rows;
+    a.n_lanes = uint32_t(n_lanes);
+    if (stack_depth > lds_rows) {
+      const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
+      c->stack_ovf.alloc(ovf_need);
+      a.stack_ovf = c->stack_ovf.p;
+    }
+    void* fn = nullptr;
+#define ZRT_TK(M) (stk16 ? reinterpret_cast<void*>(&zrt::trace_kernel<M, uint16_t>) \
+                         : reinterpret_cast<void*>(&zrt::trace_kernel<M, uint32_t>))
+    fn = mode == 0 ? ZRT_TK(0) : mode == 1 ? ZRT_TK(1) : mode == 2 ? ZRT_TK(2) : ZRT_TK(3);
+#undef ZRT_TK
+    const float* rp = d_rays.p;
+    float* tp = d_t.p;
+    int32_t* sp = d_slot.p;
+    uint32_t nn = n_rays;
+    void* args[] = {&a, &rp, &nn, &tp, &sp};
+    HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(zrt::kBlock), args, size_t(lds_rows) * zrt::kBlock * entry, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long err = 0;
+    HIPCHK(hipMemcpy(&err, c->scratch.p + zrt::kErrorSlot, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
+    std::vector<int32_t> slot(n_rays);
+    HIPCHK(hipMemcpy(out_t, d_t.p, sizeof(float) * n_rays, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(slot.data(), d_slot.p, sizeof(int32_t) * n_rays, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n_rays; ++i)
+      out_prim[i] = slot[i] < 0 ? -1 : int32_t(c->slot_to_prim[size_t(slot[i])]);
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
     return zrt::hip_fail(e);
