@@ -408,6 +408,9 @@ __device__ __forceinline__ bool order_hazard(const KArgs& a, const RayT& r, floa
 #endif
 }
 
+#ifndef ZRT_REPLAY_NARROW
+#define ZRT_REPLAY_NARROW 1  // the replay also culls boxes the ray does not cross (0: the reference's test alone)
+#endif
 #ifndef ZRT_REPLAY_INLINE
 #define ZRT_REPLAY_INLINE 1
 #endif
@@ -431,7 +434,11 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
     const int idx = sp < rows ? (int)stk[sp * kBlock] : (int)ovf[(size_t)(sp - rows) * a.n_lanes];
     const float4 lo = a.nodes[2 * idx], hi = a.nodes[2 * idx + 1];
     float e;
-    if (!box_test<false>(lo, hi, r, best_t, &e)) continue;
+    // the reference's loose test against the current best, and FAST's narrowed
+    // emptiness test (a box the ray does not cross holds no hit):
+    // left-first with the reference's t_max, so every leaf is accepted or
+    // rejected exactly as the reference does it, in ~1 % of its node visits
+    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e)) continue;
     const int left = as_int(lo.w), right = as_int(hi.w);
     if (left < 0) {
       prim_test<false, false>(a.prims, left, r, best_t, best, c_tri, c_sph);
@@ -508,7 +515,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
       if (!found) break;
     }
     // the order hazard of DESIGN.md §3, as in traverse_wide (the stack is all in LDS here)
-    if (ZRT_ORDER_EXACT && order_hazard<true>(a, r, best_t, best))
+    if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<true>(a, r, best_t, best), 0))
       reference_replay<StackT>(a, r, stk, 0u, best_t, best);
   } else {
     stk[0] = 0;
@@ -775,7 +782,7 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     ZRT_LOAD_NODE(q)
   }
 #undef ZRT_LOAD_NODE
-  if (ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best)) {
+  if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best), 0)) {  // 1e-8..1e-5 of rays
     if (STATS) ++c_replays;
 #if ZRT_REPLAY_OFF
     best_t = -best_t;  // A/B only: the replay's cost without its code (results not exact)
