@@ -443,8 +443,13 @@ def test_trace_mesh_rays_bit_exact(scenes, scene_index, rows, monkeypatch):
     targets = np.concatenate([a, (a + b) * np.float32(0.5), (a + b + c) / np.float32(3.0)]).astype(np.float32)
     o2 = np.repeat(np.asarray([s.camera.origin.x, s.camera.origin.y, s.camera.origin.z], np.float32)[None],
                    len(targets), 0) + rng.normal(scale=0.05, size=(len(targets), 3)).astype(np.float32)
-    origins = np.concatenate([o, o2]).astype(np.float32)
-    dirs = np.concatenate([d, targets - o2]).astype(np.float32)
+    # axis-aligned rays through vertices: slabs with 1/d = inf (NaN bounds) and rays
+    # running exactly along box faces and triangle edges (the narrowed test's margin)
+    kv = rng.integers(0, len(verts), 2000)
+    axis = np.eye(3, dtype=np.float32)[rng.integers(0, 3, 2000)] * rng.choice([-1, 1], (2000, 1)).astype(np.float32)
+    o3 = (verts[kv] - axis * np.float32(0.25)).astype(np.float32)
+    origins = np.concatenate([o, o2, o3]).astype(np.float32)
+    dirs = np.concatenate([d, targets - o2, axis]).astype(np.float32)
     t_ref, p_ref = O.trace(s.view, True, origins, dirs)
     assert (p_ref >= 0).mean() > 0.3
     for trav in TRAVERSALS:
