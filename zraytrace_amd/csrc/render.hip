@@ -744,10 +744,10 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
       --sp;
       next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
     }
-    // deep trees (32-bit stack): each lane walks ITS opened leaves in slot
-    // order, so lanes that opened different slots share loop trips (results
-    // are order-independent: the closest t, ties to the lower slot).  A/B: C5
-    // +2.9 %, C3 +2.2 % (not used: 16-bit stack), C4 -0.4 %.
+    // each lane walks ITS opened leaves in slot order, so lanes that opened
+    // different slots share loop trips (the result is the closest t, ties to
+    // the lower slot, order hazards flagged).  A/B against four unrolled slot
+    // blocks: C5 +2.9 %, C3 +3.2 %, C4 -0.2 % (and one copy of the tests).
     if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
       uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
       if (open != 0) {
