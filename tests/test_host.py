@@ -122,11 +122,20 @@ def test_param_validation_without_device(scenes):
     with pytest.raises(z.ZrtError) as e:
         z.render(s, cam, z.RenderParams(8, 8, 70000, 5))
     assert e.value.code == _ffi.ZRT_E_INVALID
+    with pytest.raises(z.ZrtError) as e:  # zrt_trace: unknown traversal, checked before the device
+        z.trace(s, z.RenderParams(1, 1, 1, 1, traversal=7), [[0, 0, 0]], [[0, 0, 1]])
+    assert e.value.code == _ffi.ZRT_E_INVALID
+    with pytest.raises(z.ZrtError) as e:  # zrt_render_multi: empty device list
+        z.render_multi(s, cam, z.RenderParams(8, 8, 1, 5), [])
+    assert e.value.code == _ffi.ZRT_E_INVALID
     import torch
     if not torch.cuda.is_available():
-        with pytest.raises(z.ZrtError) as e:
-            z.render(s, cam, z.RenderParams(8, 8, 1, 5))
-        assert e.value.code == _ffi.ZRT_E_NODEVICE
+        for call in (lambda: z.render(s, cam, z.RenderParams(8, 8, 1, 5)),
+                     lambda: z.render_multi(s, cam, z.RenderParams(8, 8, 1, 5), [0, 1]),
+                     lambda: z.trace(s, z.RenderParams(1, 1, 1, 1), [[0, 0, 0]], [[0, 0, 1]])):
+            with pytest.raises(z.ZrtError) as e:
+                call()
+            assert e.value.code == _ffi.ZRT_E_NODEVICE
 
 
 def test_oracle_counters_readme_rays_per_sample(scenes):
