@@ -6,11 +6,18 @@ Workload (BASELINE.json configs[3]): scene 2 of scenes.zig
 max depth 20, counter RNG seeded 42.  One step = one full frame: every rank
 renders its 8x8 tiles (tile t -> rank t % N) with the scene already resident
 in HBM, the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl")
-and assembled into the reference's framebuffer layout.  The frame is fixed as
-N grows: "scaling": "strong".
+and assembled into the reference's framebuffer layout
+(zraytrace_amd.dist.TileFrame).  The frame is fixed as N grows: "scaling":
+"strong".
 
 value = rays of all ranks (raytrace.zig:69's rays_processed, counted on the
 device) / the max-over-ranks wall time of the timed steps, in Mrays/s.
+
+roofline: the render kernel's position against every ceiling it could be
+bound by - VALU issue, L1 (TCP) accesses, L2 -> L1 lines, HBM - each
+"achieved" = a per-launch PMC count (rocprofv3 passes of this exact config,
+profiles/latest_pmc.json) / the launch's HIP-event time measured in this run;
+"bound" is the ceiling with the largest fraction.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -19,6 +26,7 @@ import argparse
 import hashlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -31,10 +39,13 @@ SCENES = {0: "manAndBall: models/Man_LOD3.obj + ground sphere", 1: "threeBalls: 
           4: "teapotAndBallCircle: teapot + ring of spheres", 5: "goat: high_poly_goat.obj + ground sphere",
           6: "texturedTeapot: the C5 substitute, 1.6 M subdivided teapot triangles + image textures"}
 # 0-5: scenes.zig:267-277; 6: DESIGN.md section 4
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
-# (SIMD-32), 2400 MHz max clock (MI355X_MICROARCH.md: CUs, max clock, SIMD/EU rows)
+
+# Ceilings.  Spec / guide values (MI355X_MICROARCH.md), replaced by the measured
+# ones of tools/ubench.hip when profiles/ubench.json holds them.
+HBM_PEAK_GBS = 8000.0  # HBM3E spec (chip-level parameters)
+# 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles x 2.4 GHz
 VALU_ISSUE_PEAK = 256 * 4 * 2400e6 / 2
+L2_PEAK_GBS = 34500.0  # L2 aggregate (guide §L2)
 
 
 def log(*a):
@@ -53,26 +64,107 @@ def algorithmic_bytes(st, n_work_units, n_pixels):
             + (st["texel_bytes"] or 12) * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of render_kernel measured by rocprofv3 PMC passes
-    (tools/gpu_profile.sh -> profiles/latest_pmc.json) for this exact config,
-    corrected as MI355X_MICROARCH.md §HBM prescribes; None if not measured."""
-    path = os.path.join(REPO, "profiles", "latest_pmc.json")
+def pmc_entry(config):
+    """The PMC record of render_kernel for this exact config (profiles/latest_pmc.json,
+    written by tools/make_latest_pmc.py from rocprofv3 --pmc passes); None if not measured."""
     try:
-        with open(path) as f:
+        with open(os.path.join(REPO, "profiles", "latest_pmc.json")) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, None
-    if d.get("config") != config:
-        return None, None
-    return d.get("hbm_bytes_per_launch"), d
+        return None
+    for e in d.get("entries", []):
+        if e.get("config") == config:
+            return e
+    return None
+
+
+def ceilings():
+    """Peak rates: measured by tools/ubench.hip on the GPU box (profiles/ubench.json) where present."""
+    c = {"valu_issue": {"peak": VALU_ISSUE_PEAK, "unit": "wave64 VALU inst/s", "source": "guide: 1024 SIMD-32 x 1/2 cyc x 2.4 GHz"},
+         "l1_access": None, "l2_lines": None,
+         "hbm": {"peak": HBM_PEAK_GBS * 1e9, "unit": "B/s", "source": "HBM3E spec (guide)"}}
+    try:
+        with open(os.path.join(REPO, "profiles", "ubench.json")) as f:
+            u = json.load(f)
+    except (OSError, ValueError):
+        u = {}
+    if u.get("valu_insts_per_s"):
+        c["valu_issue"] = {"peak": u["valu_insts_per_s"], "unit": "wave64 VALU inst/s",
+                           "source": "profiles/ubench.json (tools/ubench.hip valu_kernel, SQ_INSTS_VALU / time)"}
+    if u.get("tcp_accesses_per_s"):
+        c["l1_access"] = {"peak": u["tcp_accesses_per_s"], "unit": "TCP accesses/s",
+                          "source": "profiles/ubench.json (tools/ubench.hip load_kernel, TCP_TOTAL_CACHE_ACCESSES / time)"}
+    if u.get("tcp_tcc_read_req_per_s"):
+        c["l2_lines"] = {"peak": u["tcp_tcc_read_req_per_s"], "unit": "L1->L2 read requests/s",
+                         "source": "profiles/ubench.json (tools/ubench.hip l2 load kernel, TCP_TCC_READ_REQ / time)"}
+    else:
+        c["l2_lines"] = {"peak": L2_PEAK_GBS * 1e9 / 128, "unit": "L1->L2 read requests/s",
+                         "source": "guide L2 34.5 TB/s / 128-B lines"}
+    return c
+
+
+def roofline(pmc, kernel_s, algo_bytes, diag):
+    """Every ceiling's fraction for the launch: PMC counts per launch / the live
+    HIP-event launch time; bound = the largest fraction."""
+    out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+           "kernel_s": round(kernel_s, 6)}
+    cs = ceilings()
+    rows = {}
+    if pmc:
+        sq = pmc.get("sq") or {}
+        cache = pmc.get("cache") or {}
+        meas = {"valu_issue": sq.get("SQ_INSTS_VALU"),
+                "l1_access": cache.get("TCP_TOTAL_CACHE_ACCESSES_sum"),
+                "l2_lines": cache.get("TCP_TCC_READ_REQ_sum"),
+                "hbm": pmc.get("hbm_bytes_per_launch")}
+        for k, per_launch in meas.items():
+            if per_launch is None or cs.get(k) is None:
+                continue
+            a = per_launch / kernel_s
+            rows[k] = {"per_launch": per_launch, "achieved": a, "peak": cs[k]["peak"], "unit": cs[k]["unit"],
+                       "frac": round(a / cs[k]["peak"], 4), "peak_source": cs[k]["source"]}
+        out["traffic"] = pmc.get("hbm_bytes_per_launch")
+        out["pmc_source"] = pmc.get("source")
+        out["valu_lane_util"] = sq.get("valu_lane_util")
+        if cache.get("TCC_HIT_sum") is not None and cache.get("TCC_MISS_sum"):
+            out["l2_hit_frac"] = round(cache["TCC_HIT_sum"] / (cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"]), 4)
+    if rows:
+        b = max(rows, key=lambda k: rows[k]["frac"])
+        out.update({"bound": b, "achieved": rows[b]["achieved"], "peak": rows[b]["peak"], "unit": rows[b]["unit"],
+                    "frac": rows[b]["frac"]})
+        if "hbm" in rows:
+            out["hbm_gbs_measured"] = round(rows["hbm"]["achieved"] / 1e9, 1)
+            out["hbm_frac"] = rows["hbm"]["frac"]
+    out["ceilings"] = rows
+    rays = max(1, diag["rays_processed"])
+    out["algorithmic"] = {
+        "bytes_per_launch": int(algo_bytes), "gbs": round(algo_bytes / kernel_s / 1e9, 1),
+        "note": "bytes each ray's node/primitive/material reads and path-state writes touch; served by L1/L2 "
+                "(the bunny scene is ~2 MB), so this is not an HBM figure and carries no HBM fraction",
+        "per_ray": {"node_visits": round(diag["node_visits"] / rays, 2),
+                    "leaf_visits": round(diag["leaf_visits"] / rays, 2),
+                    "prim_tests": round(diag["prim_tests"] / rays, 2),
+                    "bytes": round(algo_bytes / rays, 1)}}
+    return out
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(scene, scene_index, depth):
     """The oracle (single-threaded C restatement, reference RNG stream) on a
     bounded sample of the same scene at the bench's depth: 128x128 @ 4 spp, or
     16x16 @ 1 spp for a mesh of > 100k primitives (the reference's loose slab
-    test makes its traversal cost grow with the tree)."""
+    test makes its traversal cost grow with the tree).  Also config C1 in full
+    (scene 1, 256x256 @ 16 spp, depth 30: BASELINE.md §3)."""
     import zraytrace_amd as z
     from oracle import oracle_py as O
     big = scene.view.contents.n_prims > 100_000
@@ -81,11 +173,35 @@ def cpu_baseline(scene, scene_index, depth):
     p = z.RenderParams(w, h, spp, depth, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
     _, st = O.render(scene.view, scene.camera, p)
     dt = st["render_ms"] / 1e3  # the sampling loop only; its BVH build is timed apart (raytrace.zig:150)
+    s1 = z.load_scene(1)
+    _, c1 = O.render(s1.view, s1.camera, z.RenderParams(256, 256, 16, 30, rng_mode=z.ZRT_RNG_REFERENCE_STREAM))
+    c1_s = c1["render_ms"] / 1e3
     return {"value": st["rays_processed"] / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"oracle/ (C restatement of the Zig path, reference RNG stream), scene {scene_index} "
                       f"({SCENES[scene_index].split(':')[0]}), {w}x{h} @ {spp} spp, depth {depth}: "
-                      f"{st['rays_processed']} rays in {dt:.2f} s on 1 core ({os.cpu_count()} visible; "
-                      f"BVH build {st['preprocess_ms'] / 1e3:.2f} s excluded)"}
+                      f"{st['rays_processed']} rays in {dt:.2f} s on 1 core (BVH build "
+                      f"{st['preprocess_ms'] / 1e3:.2f} s excluded)",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "c1_full": {"config": "scene 1 (7 spheres, list), 256x256 @ 16 spp, depth 30, reference RNG stream",
+                        "rays": c1["rays_processed"], "seconds": round(c1_s, 3),
+                        "mrays_per_s": round(c1["rays_processed"] / c1_s / 1e6, 3), "cores": 1}}
+
+
+def reference_check(frame_obj, params, fast_sha1, z):
+    """One untimed launch of the same frame with the REFERENCE traversal (the
+    reference's left-first DFS and loose slab test, bvh.zig:187-205): its rate
+    separates the algorithm from the hardware, and its frame must hash equal to
+    FAST's (the exactness claim of DESIGN.md §3 at the full bench size)."""
+    pref = z.RenderParams(**{**params.__dict__, "traversal": z.ZRT_TRAVERSAL_REFERENCE})
+    t = time.perf_counter()
+    kms = frame_obj.step(pref)
+    st = frame_obj.ctx.stats()
+    img = frame_obj.image()
+    wall = time.perf_counter() - t
+    sha = hashlib.sha1(img.tobytes()).hexdigest()
+    return {"traversal": "reference", "mrays_per_s": round(st["rays_processed"] / (st["render_ms"] / 1e3) / 1e6, 2),
+            "kernel_ms": round(kms, 2), "render_ms": round(st["render_ms"], 2), "wall_s": round(wall, 2),
+            "rays": st["rays_processed"], "frame_sha1": sha, "frame_equal_to_fast": sha == fast_sha1}
 
 
 def main():
@@ -101,6 +217,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--traversal", choices=["fast", "reference", "binary"], default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reference-check", action="store_true",
+                    help="skip the untimed REFERENCE-traversal launch of the same frame (N=1 only)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK)")
@@ -124,31 +242,17 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     import zraytrace_amd as z
+    from zraytrace_amd.dist import TileFrame
     scene = z.load_scene(args.scene)
     trav = {"fast": z.ZRT_TRAVERSAL_FAST, "reference": z.ZRT_TRAVERSAL_REFERENCE,
             "binary": z.ZRT_TRAVERSAL_BINARY}[args.traversal]
     params = z.RenderParams(args.width, args.height, args.spp, args.depth, traversal=trav,
                             rank=rank, world_size=world, device=local, sample_chunk=args.chunk)
-    ctx = z.RenderContext(scene, params)
-    from zraytrace_amd.dist import gather_tiles, tile_counts
-    counts = tile_counts(params)
-    my_tiles, max_tiles = counts[rank], max(counts)
-    tiles = torch.zeros(max_tiles * 64 * 3, dtype=torch.float32, device="cuda")
-    frame = torch.empty(args.height * args.width * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
-    p0 = z.RenderParams(**{**params.__dict__, "rank": 0})
-    stream = torch.cuda.current_stream().cuda_stream
-
-    def step():
-        ctx.render_tiles(scene.camera, params, tiles.data_ptr(), stream)
-        kms = ctx.kernel_ms()  # HIP events around the kernel, on its launch stream
-        gathered = gather_tiles(tiles, counts, rank, world, dst=0)  # RCCL over xGMI
-        if rank == 0:
-            ctx.assemble(p0, gathered.data_ptr(), frame.data_ptr(), stream)
-        return kms
+    fr = TileFrame(scene, params, rank, world)
 
     for i in range(args.warmup):
         t = time.perf_counter()
-        step()
+        fr.step()
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f} s")
 
@@ -158,20 +262,19 @@ def main():
     t0 = time.perf_counter()
     kernel_ms = []
     for i in range(args.steps):
-        kernel_ms.append(step())
+        kernel_ms.append(fr.step())
         log(f"[rank {rank}] step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    st = ctx.stats()  # Progress counters of the last timed launch (identical every step)
+    st = fr.ctx.stats()  # Progress counters of the last timed launch (identical every step)
+    frame_sha1 = hashlib.sha1(fr.image().tobytes()).hexdigest() if rank == 0 else None
     # Traffic diagnostics (node visits, primitive tests, ...) come from one extra,
     # untimed launch of the diagnostic kernel flavour: same traversal, same image.
-    pdiag = z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS})
-    ctx.render_tiles(scene.camera, pdiag, tiles.data_ptr(), stream)
-    diag = ctx.stats()
-    diag_kernel_ms = ctx.kernel_ms()
+    diag_kernel_ms = fr.step(z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS}))
+    diag = fr.ctx.stats()
     assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
     red = "cuda" if args.dist_backend == "nccl" else "cpu"
     rays = torch.tensor([float(st["rays_processed"]), float(st["samples_processed"])], dtype=torch.float64,
@@ -184,19 +287,16 @@ def main():
     elapsed = el.item()
 
     if rank == 0:
-        # hash of the last timed step's assembled frame: identical for every N
-        frame_sha1 = hashlib.sha1(frame.cpu().numpy().tobytes()).hexdigest()
         value = total_rays * args.steps / elapsed / 1e6
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
         chunk = args.chunk or 32  # ZRT_DEFAULT_SAMPLE_CHUNK
-        n_units = my_tiles * 64 * ((args.spp + chunk - 1) // chunk)
+        n_units = fr.counts[rank] * ((args.spp + chunk - 1) // chunk)
         algo = algorithmic_bytes(diag, n_units, diag["pixels_processed"])
-        achieved = algo / avg_kernel_s / 1e9
         pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
-        traffic, pmc = pmc_traffic(pmc_key)
-        traffic_src = pmc.get("source") if pmc else None
-        sq = (pmc or {}).get("sq") or {}
+        roof = roofline(pmc_entry(pmc_key) if world == 1 else None, avg_kernel_s, algo, diag)
+        roof["kernel"] = f"render_kernel (BVH {args.traversal} traversal)"
+        roof["counters_from"] = f"one untimed ZRT_FLAG_STATS launch (kernel {diag_kernel_ms:.1f} ms)"
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -221,45 +321,22 @@ def main():
             "samples_per_step": int(total_samples),
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 4),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_unit": "bytes per launch (rocprofv3 (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB)",
-                         "traffic_source": traffic_src,
-                         # the metric's "achieved HBM GB/s": measured HBM bytes per launch over the
-                         # launch time (frac_measured against the 8 TB/s peak)
-                         "hbm_gbs_measured": (round(traffic / avg_kernel_s / 1e9, 1) if traffic else None),
-                         "frac_measured": (round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
-                         "kernel": f"render_kernel (BVH {args.traversal} traversal)",
-                         "algorithmic_bytes_per_launch": int(algo),
-                         "per_ray": {"node_visits": round(diag["node_visits"] / max(1, diag["rays_processed"]), 2),
-                                     "leaf_visits": round(diag["leaf_visits"] / max(1, diag["rays_processed"]), 2),
-                                     "prim_tests": round(diag["prim_tests"] / max(1, diag["rays_processed"]), 2),
-                                     "bytes": round(algo / max(1, diag["rays_processed"]), 1)},
-                         "counters_from": "one untimed ZRT_FLAG_STATS launch (kernel "
-                                          f"{diag_kernel_ms:.1f} ms)",
-                         "note": "algorithmic bytes are what each ray's node/primitive/material reads and "
-                                 "path-state writes touch; the scene (~0.5 MB for the bunny) is L1/L2-resident, "
-                                 "so they are served by the caches and frac > 1 against HBM means the loop is not "
-                                 "HBM-bound (traffic = what actually reached HBM). The binding limits are "
-                                 "dependent-load latency and VALU issue (DESIGN.md section 4); see valu_*.",
-                         "valu_lane_util": sq.get("valu_lane_util"),
-                         "valu_insts_per_ray": (round(sq["SQ_INSTS_VALU"] / max(1, st["rays_processed"]), 2)
-                                                if sq.get("SQ_INSTS_VALU") else None),
-                         # the bound this loop actually sits against: wave64 VALU instructions issued
-                         # per second over the chip's issue peak (same PMC pass and its duration)
-                         "valu_issue_frac": (round(sq["SQ_INSTS_VALU"] / (pmc["duration_ns"] * 1e-9) / VALU_ISSUE_PEAK, 4)
-                                             if sq.get("SQ_INSTS_VALU") and pmc.get("duration_ns") else None)},
+            "order_replays": diag["order_replays"],
+            "roofline": roof,
             "accel": {"reference_bvh_nodes": diag["bvh_nodes"], "reference_bvh_depth": diag["bvh_max_depth"],
                       "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
             "frame_sha1": frame_sha1,
         }
+        if world == 1 and args.traversal == "fast" and st["used_bvh"] and not args.no_reference_check:
+            log("[rank 0] reference-traversal launch of the same frame ...")
+            out["reference_traversal"] = reference_check(fr, params, frame_sha1, z)
         if world == 1 and not args.no_cpu_baseline:
             log("[rank 0] cpu baseline (oracle, 1 core) ...")
             out["cpu_baseline"] = cpu_baseline(scene, args.scene, args.depth)
         print(json.dumps(out), flush=True)
 
-    ctx.close()
+    fr.close()
     if world > 1:
         dist.destroy_process_group()
 

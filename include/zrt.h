@@ -228,6 +228,21 @@ int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera,
                      const zrt_params* params, const uint32_t* devices,
                      uint32_t n_devices, float* out_rgb, zrt_stats* stats);
 
+/* zrt_render_multi split into a persistent multi-GPU context (a Zig host
+ * rendering many frames of one scene): zrt_multi_create builds the BVH once,
+ * uploads the scene to every device of the list and creates the RCCL
+ * communicators once (one rank per distinct device, >= 2 devices; otherwise
+ * the tiles move by device copies and RCCL is not loaded).
+ * zrt_multi_render renders one frame as zrt_render_multi does (same image,
+ * same stats); params->rank / world_size / device are ignored and
+ * params->bounded_volume_hierarchy must imply the create-time BVH decision. */
+typedef struct zrt_multi zrt_multi;
+int zrt_multi_create(const zrt_scene* scene, const zrt_params* params,
+                     const uint32_t* devices, uint32_t n_devices, zrt_multi** out);
+int zrt_multi_render(zrt_multi* multi, const zrt_camera* camera,
+                     const zrt_params* params, float* out_rgb, zrt_stats* stats);
+int zrt_multi_destroy(zrt_multi* multi);
+
 /* The closest-hit query of one rayColor step (raytrace.zig:71-81: the top-level
  * surfaces tested with t_min = 0.001 and a shrinking t_max; under BVH that is
  * BVHNode.hit, bvh.zig:187-205) for a batch of rays on params->device, through
@@ -267,12 +282,24 @@ int zrt_ctx_destroy(zrt_ctx* ctx);
 int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n_tiles);
 
 /* Render this rank's tiles into dev_tiles (device pointer, tile-major,
- * n_tiles*64*3 f32) on `hip_stream` (hipStream_t, NULL = default stream).
- * Asynchronous: returns after enqueueing; counters are produced by
- * zrt_ctx_stats after the stream is synchronised. */
+ * n_tiles*64*3 f32) on `hip_stream` (a hipStream_t; NULL = the context's own
+ * stream, a blocking stream, so work the caller later enqueues on the legacy
+ * default stream waits for it).  Asynchronous: returns after enqueueing.
+ * zrt_ctx_sync / zrt_ctx_stats / zrt_ctx_last_kernel_ms wait for the launch
+ * (on whichever stream it ran) and return ZRT_E_UNSUPPORTED if the device
+ * reported an error (a traversal stack overflow); such a launch also writes
+ * NaN to every pixel of dev_tiles, and the next zrt_ctx_render_tiles on the
+ * context returns the error if the launch has finished by then.
+ * params->device must be the context's device, and params->
+ * bounded_volume_hierarchy must imply the BVH decision the context was built
+ * with (ZRT_E_INVALID otherwise). */
 int zrt_ctx_render_tiles(zrt_ctx* ctx, const zrt_camera* camera,
                          const zrt_params* params, float* dev_tiles,
                          void* hip_stream);
+
+/* Wait for the context's last launch; ZRT_OK, or ZRT_E_UNSUPPORTED when the
+ * device reported an error during it (see zrt_ctx_render_tiles). */
+int zrt_ctx_sync(zrt_ctx* ctx);
 
 /* Scatter gathered tiles of all ranks (rank-major: rank r's n_tiles(r) tiles
  * follow rank r-1's) into the framebuffer layout of raytrace.zig:182.
@@ -280,7 +307,14 @@ int zrt_ctx_render_tiles(zrt_ctx* ctx, const zrt_camera* camera,
 int zrt_ctx_assemble(zrt_ctx* ctx, const zrt_params* params,
                      const float* dev_gathered, float* dev_frame, void* hip_stream);
 
-/* Counters of the last zrt_ctx_render_tiles (synchronises the ctx stream). */
+/* The same from the layout a gather of equal per-rank counts produces: rank r's
+ * tiles start at tile r * stride_tiles (stride_tiles >= every rank's count;
+ * the tiles past a rank's count are padding and are not read). */
+int zrt_ctx_assemble_padded(zrt_ctx* ctx, const zrt_params* params,
+                            const float* dev_gathered, uint32_t stride_tiles,
+                            float* dev_frame, void* hip_stream);
+
+/* Counters of the last zrt_ctx_render_tiles (waits for that launch). */
 int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
 
 /* Raw device counter slots of the last launch (diagnostics; n <= 24):

@@ -20,23 +20,27 @@ from zraytrace_amd.dist import gather_tiles, tile_counts
 
 
 def assemble_numpy(gathered, counts, width, height, world):
-    """Restatement of assemble_kernel (render.hip) for the test."""
+    """Restatement of assemble_kernel's padded mode (render.hip) for the test:
+    rank r's tiles start at tile r * max(counts); tiles past a rank's count are padding."""
     xbound = height                      # raytrace.zig:168
     tiles_x = (xbound + 7) // 8
+    n_tiles = tiles_x * ((height + 7) // 8)
+    stride = max(counts) * 64
     frame = np.zeros((height, width, 3), np.float32)
     owner = np.full((height, width), -1, np.int64)
-    base = 0
-    for r in range(world):
-        for w in range(counts[r] * 64):
-            lt, p = divmod(w, 64)
-            t = lt * world + r
-            px = (t % tiles_x) * 8 + p % 8
-            py = (t // tiles_x) * 8 + p // 8
-            if px < xbound and py < height:
-                assert owner[py, px] == -1, "pixel assembled twice"
-                owner[py, px] = r
-                frame[py, px] = gathered[base + w]
-        base += counts[r] * 64
+    for i in range(world * stride):
+        r, w = divmod(i, stride)
+        lt, p = divmod(w, 64)
+        t = lt * world + r
+        if t >= n_tiles:
+            assert lt >= counts[r], "a rank's own tile treated as padding"
+            continue
+        px = (t % tiles_x) * 8 + p % 8
+        py = (t // tiles_x) * 8 + p // 8
+        if px < xbound and py < height:
+            assert owner[py, px] == -1, "pixel assembled twice"
+            owner[py, px] = r
+            frame[py, px] = gathered[i]
     return frame, owner
 
 
@@ -79,7 +83,7 @@ def test_gloo_gather_and_assemble(world, width, height):
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    assert len(gathered) == sum(counts) * 64
+    assert len(gathered) == world * max(counts) * 64
     frame, owner = assemble_numpy(gathered, counts, width, height, world)
     xb = height
     assert (owner[:, :xb] >= 0).all() and (owner[:, xb:] == -1).all()

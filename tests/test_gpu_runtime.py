@@ -1,0 +1,194 @@
+"""GPU tests of the runtime around the kernel: device-error surfacing, stream
+semantics of the C ABI, the persistent multi-GPU context, and bench.py's N-rank
+step (render_tiles -> gather -> assemble) end to end.
+
+Run on an MI355X: ``pytest -m gpu``.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import zraytrace_amd as z
+from oracle import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+COUNTERS = ("recursion_depth_hits", "reflections", "background_hits", "rays_processed",
+            "pixels_processed", "samples_processed")
+
+
+def same_bits(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return ((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))).all()
+
+
+# ---- device errors surface without a stats call (raytrace.zig:136-138's error union) ---
+
+@pytest.mark.parametrize("traversal", [z.ZRT_TRAVERSAL_FAST, z.ZRT_TRAVERSAL_REFERENCE, z.ZRT_TRAVERSAL_BINARY],
+                         ids=["fast", "reference", "binary"])
+def test_stack_overflow_is_an_error(scenes, traversal, monkeypatch):
+    """A traversal stack too small for the tree (forced by ZRT_DEBUG_STACK_CAP):
+    zrt_render returns ZRT_E_UNSUPPORTED instead of a silently wrong frame."""
+    monkeypatch.setenv("ZRT_DEBUG_STACK_CAP", "4")
+    s = scenes(3)  # teapot: reference BVH depth > 4
+    with pytest.raises(z.ZrtError) as e:
+        z.render(s, s.camera, z.RenderParams(32, 32, 2, 8, traversal=traversal))
+    assert e.value.code == z._ffi.ZRT_E_UNSUPPORTED
+    assert "overflow" in str(e.value)
+
+
+def test_stack_overflow_context_path(scenes, monkeypatch):
+    """The asynchronous path: the launch's tiles are NaN, zrt_ctx_sync reports the
+    error, and a caller that never synchronises through the ABI gets it from the
+    next zrt_ctx_render_tiles (once); after that the context renders correctly."""
+    import torch
+    s = scenes(3)
+    p = z.RenderParams(32, 32, 2, 8)
+    ctx = z.RenderContext(s, p)
+    buf = torch.zeros(ctx.tile_count(p) * 64 * 3, dtype=torch.float32, device="cuda")
+    monkeypatch.setenv("ZRT_DEBUG_STACK_CAP", "4")
+    ctx.render_tiles(s.camera, p, buf.data_ptr())
+    with pytest.raises(z.ZrtError) as e:
+        ctx.sync()
+    assert e.value.code == z._ffi.ZRT_E_UNSUPPORTED
+    assert torch.isnan(buf).all()
+    # a caller that skipped sync: the next launch reports the finished one's error, once
+    ctx.render_tiles(s.camera, p, buf.data_ptr())
+    torch.cuda.synchronize()
+    monkeypatch.delenv("ZRT_DEBUG_STACK_CAP")
+    with pytest.raises(z.ZrtError) as e:
+        ctx.render_tiles(s.camera, p, buf.data_ptr())
+    assert e.value.code == z._ffi.ZRT_E_UNSUPPORTED
+    ctx.render_tiles(s.camera, p, buf.data_ptr())
+    ctx.sync()
+    assert torch.isfinite(buf).all()
+    ctx.close()
+
+
+def test_render_tiles_rejects_mismatched_params(scenes):
+    s = scenes(2)
+    p = z.RenderParams(16, 16, 1, 4)
+    ctx = z.RenderContext(s, p)
+    import torch
+    buf = torch.zeros(ctx.tile_count(p) * 64 * 3, dtype=torch.float32, device="cuda")
+    for bad in (z.RenderParams(16, 16, 1, 4, device=1), z.RenderParams(16, 16, 1, 4, bounded_volume_hierarchy=False)):
+        with pytest.raises(z.ZrtError) as e:
+            ctx.render_tiles(s.camera, bad, buf.data_ptr())
+        assert e.value.code == z._ffi.ZRT_E_INVALID
+    ctx.close()
+
+
+# ---- stream semantics (zrt.h: NULL = the context's blocking stream) ----------------
+
+def test_null_stream_orders_before_torch_default_stream(scenes):
+    """Tiles rendered on the NULL stream (the context's own, blocking stream) are
+    complete when the next work on torch's default (legacy) stream reads them,
+    with no host synchronisation in between."""
+    import torch
+    s = scenes(2)
+    p = z.RenderParams(256, 256, 64, 20)
+    ref, _ = z.render(s, s.camera, p)
+    ctx = z.RenderContext(s, p)
+    n = ctx.tile_count(p)
+    tiles = torch.full((n * 64 * 3,), -1.0, dtype=torch.float32, device="cuda")
+    frame = torch.empty(256 * 256 * 3, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        tiles.fill_(-1.0)
+        ctx.render_tiles(s.camera, p, tiles.data_ptr(), 0)
+        copy = tiles.clone()  # torch's default stream: must see the finalized tiles
+        ctx.assemble(p, copy.data_ptr(), frame.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert same_bits(frame.cpu().numpy().reshape(256, 256, 3), ref)
+    ctx.close()
+
+
+# ---- persistent multi-GPU context ----------------------------------------------------
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_context_frames(scenes, devices):
+    """zrt_multi_*: scene uploaded once, several frames with different params;
+    every frame equals zrt_render's (and counters sum to it)."""
+    s = scenes(2)
+    m = z.MultiContext(s, z.RenderParams(40, 40, 4, 20), devices)
+    for w, h, spp in ((40, 40, 4), (24, 16, 8), (40, 40, 4)):
+        p = z.RenderParams(w, h, spp, 20)
+        one, st1 = z.render(s, s.camera, p)
+        img, stm = m.render(s.camera, p)
+        assert same_bits(one, img)
+        for k in COUNTERS:
+            assert st1[k] == stm[k], k
+        assert stm["n_gpus"] == 1
+    m.close()
+
+
+def test_multi_render_surfaces_device_error(scenes, monkeypatch):
+    monkeypatch.setenv("ZRT_DEBUG_STACK_CAP", "4")
+    s = scenes(3)
+    with pytest.raises(z.ZrtError) as e:
+        z.render_multi(s, s.camera, z.RenderParams(24, 24, 1, 6), [0, 0])
+    assert e.value.code == z._ffi.ZRT_E_UNSUPPORTED
+
+
+# ---- bench.py's N-rank step, end to end ---------------------------------------------
+
+def _free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def _rank_worker(rank, world, port, scene_index, dims, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import zraytrace_amd as zz
+        from zraytrace_amd.dist import TileFrame
+        s = zz.load_scene(scene_index)
+        w, h, spp, depth = dims
+        p = zz.RenderParams(w, h, spp, depth, rank=rank, world_size=world, device=0)
+        fr = TileFrame(s, p, rank, world)
+        for _ in range(2):  # the buffers are reused across steps
+            fr.step()
+        st = fr.ctx.stats()
+        img = fr.image() if rank == 0 else None
+        q.put((rank, img, {k: st[k] for k in COUNTERS}))
+        fr.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tileframe_ranks_end_to_end(scenes, world):
+    """world gloo ranks sharing GPU 0 run bench.py's step (TileFrame: render_tiles
+    on an explicit stream -> padded gather -> assemble_padded): rank 0's frame
+    equals zrt_render's and the oracle's bit for bit, and the ranks' counters sum
+    to zrt_render's."""
+    import torch.multiprocessing as mp
+    dims = (40, 40, 4, 20)
+    s = scenes(2)
+    p = z.RenderParams(*dims)
+    one, st1 = z.render(s, s.camera, p)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, 2, dims, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    img = next(g[1] for g in got if g[0] == 0)
+    assert same_bits(img, one)
+    ref, _ = O.render(s.view, s.camera, p)
+    assert same_bits(img, ref)
+    for k in COUNTERS:
+        assert sum(g[2][k] for g in got) == st1[k], k

@@ -130,6 +130,39 @@ def render_multi(scene, camera: _ffi.Camera, params: RenderParams, devices):
     return out, st.as_dict()
 
 
+class MultiContext:
+    """Persistent multi-GPU context (zrt_multi_*): scene on every device of the
+    list, RCCL communicators created once; render() = zrt_render_multi's frame."""
+
+    def __init__(self, scene, params: RenderParams, devices):
+        view = scene.view if isinstance(scene, LoadedScene) else scene
+        self._scene = scene
+        h = C.c_void_p()
+        p = params.abi()
+        devs = (C.c_uint32 * len(devices))(*devices)
+        check(lib().zrt_multi_create(view, C.byref(p), devs, len(devices), C.byref(h)))
+        self._h = h
+
+    def render(self, camera, params: RenderParams):
+        out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+        st = _ffi.Stats()
+        p = params.abi()
+        check(lib().zrt_multi_render(self._h, C.byref(camera), C.byref(p),
+                                     out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+        return out, st.as_dict()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().zrt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def trace(scene, params: RenderParams, origins, directions):
     """Closest hit of each ray (zrt_trace): (t float32[n], +inf on a miss; prim int32[n], -1 on a miss)."""
     view = scene.view if isinstance(scene, LoadedScene) else scene
@@ -170,6 +203,17 @@ class RenderContext:
         p = params.abi()
         check(lib().zrt_ctx_assemble(self._h, C.byref(p), C.c_void_p(dev_gathered),
                                      C.c_void_p(dev_frame), C.c_void_p(stream or None)))
+
+    def sync(self):
+        """Wait for the last launch; raises ZrtError on a device error (zrt_ctx_sync)."""
+        check(lib().zrt_ctx_sync(self._h))
+
+    def assemble_padded(self, params: RenderParams, dev_gathered: int, stride_tiles: int, dev_frame: int,
+                        stream: int = 0):
+        """Assemble from a gather of equal per-rank counts: rank r at tile r * stride_tiles."""
+        p = params.abi()
+        check(lib().zrt_ctx_assemble_padded(self._h, C.byref(p), C.c_void_p(dev_gathered), stride_tiles,
+                                            C.c_void_p(dev_frame), C.c_void_p(stream or None)))
 
     def stats(self) -> dict:
         st = _ffi.Stats()

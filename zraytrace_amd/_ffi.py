@@ -109,6 +109,11 @@ SIGNATURES = [
                              C.POINTER(C.c_float), C.POINTER(Stats)]),
     ("zrt_render_multi", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                                    C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_float), C.POINTER(Stats)]),
+    ("zrt_multi_create", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_uint32), C.c_uint32,
+                                   C.POINTER(_P)]),
+    ("zrt_multi_render", C.c_int, [_P, C.POINTER(Camera), C.POINTER(Params), C.POINTER(C.c_float),
+                                   C.POINTER(Stats)]),
+    ("zrt_multi_destroy", C.c_int, [_P]),
     ("zrt_trace", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_float), C.c_uint32,
                             C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -122,6 +127,8 @@ SIGNATURES = [
     ("zrt_ctx_tile_count", C.c_int, [_P, C.POINTER(Params), C.POINTER(C.c_uint32)]),
     ("zrt_ctx_render_tiles", C.c_int, [_P, C.POINTER(Camera), C.POINTER(Params), _P, _P]),
     ("zrt_ctx_assemble", C.c_int, [_P, C.POINTER(Params), _P, _P, _P]),
+    ("zrt_ctx_assemble_padded", C.c_int, [_P, C.POINTER(Params), _P, C.c_uint32, _P, _P]),
+    ("zrt_ctx_sync", C.c_int, [_P]),
     ("zrt_ctx_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("zrt_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("zrt_ctx_debug_counters", C.c_int, [_P, C.POINTER(C.c_uint64), C.c_uint32]),

@@ -488,9 +488,8 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         if (hl && hr) {
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
-          if (sp < cap) stk[sp * stride] = (StackT)far_idx;
-          else atomicOr(a.error_flag, 1u);
-          ++sp;
+          if (sp < cap) stk[(sp++) * stride] = (StackT)far_idx;
+          else atomicOr(a.error_flag, 1u);  // too deep for the stack: the subtree is dropped (flagged)
           left = rfirst ? as_int(r0.w) : as_int(l0.w);
           right = rfirst ? as_int(r1.w) : as_int(l1.w);
           continue;
@@ -502,7 +501,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
       bool found = false;
       while (sp > 0) {
         --sp;
-        const int idx = sp < cap ? stk[sp * stride] : 0;
+        const int idx = stk[sp * stride];
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
         if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * 1.0000153f, &e)) {
@@ -724,21 +723,24 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
       // three stores are unconditional (entries above the new top are dead)
       const StackT e0 = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1), e1 = (StackT)(n == 4 ? r2 : r1);
       const StackT e2 = (StackT)r1;
+      // sp <= cap - 3 always holds (the clamp below), so the three stores stay in the rows
       if (sp + 3 <= rows) {
         stk[sp * stride] = e0;
         stk[(sp + 1) * stride] = e1;
         stk[(sp + 2) * stride] = e2;
-      } else if (sp + 3 <= cap) {  // deep trees: rows past the LDS part live in global memory
+      } else if (kOvf) {  // deep trees: rows past the LDS part live in global memory
         const StackT e[3] = {e0, e1, e2};
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
           if (sp + j < rows) stk[(sp + j) * stride] = e[j];
           else ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
         }
-      } else {
-        atomicOr(a.error_flag, 1u);
       }
-      sp = min(sp + n - 1, cap - 3);
+      const uint32_t nsp = sp + n - 1;
+      // the host sizes cap = the tree's deepest stack + 3, so this never fires
+      // unless the stack was sized too small: then entries would be lost
+      if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, 1u);
+      sp = min(nsp, cap - 3);
       next = r0;
     } else if (sp != 0) {
       --sp;
@@ -1203,10 +1205,14 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
 }
 
 // Per-pixel sum of the chunk sums in chunk order, times 1/spp
-// (raytrace.zig:182), into the rank's tile-major output.
+// (raytrace.zig:182), into the rank's tile-major output.  A launch that set the
+// device error flag (a traversal stack overflow) leaves NaN in every pixel, so
+// a caller that never asks for the status still cannot take the frame for a
+// correct one (the status itself: zrt_ctx_sync / zrt_ctx_stats / zrt_render).
 __global__ void finalize_kernel(const float4* __restrict__ partial, float* __restrict__ out,
                                 uint32_t n_slots, uint32_t n_chunks, uint32_t world, uint32_t rank,
-                                uint32_t tiles_x, uint32_t xbound, uint32_t height, float color_scale) {
+                                uint32_t tiles_x, uint32_t xbound, uint32_t height, float color_scale,
+                                const unsigned long long* __restrict__ error_flag) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_slots) return;
   const uint32_t lt = i >> 6, p = i & 63u;
@@ -1214,7 +1220,9 @@ __global__ void finalize_kernel(const float4* __restrict__ partial, float* __res
   const uint32_t px = (t % tiles_x) * 8u + (p & 7u);
   const uint32_t py = (t / tiles_x) * 8u + (p >> 3);
   float r = 0.0f, g = 0.0f, b = 0.0f;
-  if (px < xbound && py < height) {
+  if (*error_flag != 0ull) {
+    r = g = b = __builtin_nanf("");
+  } else if (px < xbound && py < height) {
     for (uint32_t j = 0; j < n_chunks; ++j) {  // [chunk][slot]: a wave reads 1 KiB per chunk
       const float4 v = partial[(size_t)j * n_slots + i];
       r += v.x;
@@ -1231,18 +1239,26 @@ __global__ void finalize_kernel(const float4* __restrict__ partial, float* __res
 }
 
 // Scatter gathered rank tiles into the framebuffer (raytrace.zig:182 layout).
+// Packed (stride_px == 0): rank r's tiles start at rank_base[r].  Padded: rank r
+// starts at r * stride_px, as a gather of equal per-rank counts leaves them.
 __global__ void assemble_kernel(const float* __restrict__ gathered, float* __restrict__ frame,
                                 const uint32_t* __restrict__ rank_base, uint32_t world,
                                 uint32_t tiles_x, uint32_t xbound, uint32_t height, uint32_t width,
-                                uint32_t total) {
+                                uint32_t total, uint32_t stride_px, uint32_t n_tiles) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  // find the rank owning gathered pixel i (world is small)
-  uint32_t r = 0;
-  while (r + 1 < world && rank_base[r + 1] <= i) ++r;
-  const uint32_t w = i - rank_base[r];
+  uint32_t r = 0, w = 0;
+  if (stride_px) {
+    r = i / stride_px;
+    w = i - r * stride_px;
+  } else {
+    // find the rank owning gathered pixel i (world is small)
+    while (r + 1 < world && rank_base[r + 1] <= i) ++r;
+    w = i - rank_base[r];
+  }
   const uint32_t lt = w >> 6, p = w & 63u;
   const uint32_t t = lt * world + r;
+  if (t >= n_tiles) return;  // padding
   const uint32_t px = (t % tiles_x) * 8u + (p & 7u);
   const uint32_t py = (t / tiles_x) * 8u + (p >> 3);
   if (px >= xbound || py >= height) return;
@@ -1303,6 +1319,10 @@ struct DevBuf {
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) {
+    o.p = nullptr;
+    o.n = 0;
+  }
   ~DevBuf() { release(); }
   void release() {
     if (p) (void)hipFree(p);
@@ -1340,6 +1360,9 @@ int check_device(int dev) {
 int validate_scene(const zrt_scene* s) {
   if (!s) return fail(ZRT_E_INVALID, "scene is null");
   if (s->n_prims && !s->prims) return fail(ZRT_E_INVALID, "prims is null");
+  if (s->n_materials && !s->materials) return fail(ZRT_E_INVALID, "materials is null");
+  if (s->n_textures && !s->textures) return fail(ZRT_E_INVALID, "textures is null");
+  if (s->n_images && !s->images) return fail(ZRT_E_INVALID, "images is null");
   if (s->n_prims >= (1u << 29)) return fail(ZRT_E_UNSUPPORTED, "more than 2^29 primitives");
   for (uint32_t i = 0; i < s->n_prims; ++i) {
     const zrt_prim& p = s->prims[i];
@@ -1428,9 +1451,12 @@ struct zrt_ctx {
   zrt::DevBuf<unsigned long long> wave_times;  // ZRT_PROFILE builds
   uint32_t n_waves = 0;
   bool scheduled = false;
-  hipEvent_t ev_pre = nullptr, ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_pre = nullptr, ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
   double preprocess_ms = 0, upload_ms = 0;
-  // last launch
+  // last launch: its device error flag, copied into pinned host memory behind
+  // ev_done on the stream it was enqueued on (the caller's, or `stream`)
+  unsigned long long* err_host = nullptr;
+  bool err_reported = false;  // the last launch's device error was returned to the caller
   uint32_t last_pixels = 0, last_spp = 0, launched = 0;
   bool last_stats = false;
   int last_mode = 0;
@@ -1439,6 +1465,8 @@ struct zrt_ctx {
     if (ev_pre) (void)hipEventDestroy(ev_pre);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+    if (err_host) (void)hipHostFree(err_host);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -1728,7 +1756,7 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.partial = c->probe_partial.p;
   pa.counters = c->probe_scratch.p;
   pa.work_counter = reinterpret_cast<uint32_t*>(c->probe_scratch.p + kWorkSlot);
-  pa.error_flag = reinterpret_cast<uint32_t*>(c->probe_scratch.p + kErrorSlot);
+  // pa.error_flag stays the render launch's: a probe overflow fails the frame too
   pa.unit_cost = c->tile_cost.p;
   pa.tile_order = nullptr;
   const uint32_t pgrid = std::max(1u, std::min(grid, (my_tiles + kBlock / 64 - 1) / (kBlock / 64)));
@@ -1749,6 +1777,36 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
 
 int hip_fail(const HipError& e) {
   return fail(ZRT_E_HIP, e.where + ": " + hipGetErrorString(e.err));
+}
+
+// The catch clauses of every C entry point: no exception crosses the ABI.
+#define ZRT_CATCH_ALL                                  \
+  catch (const ::zrt::HipError& e) {                   \
+    return ::zrt::hip_fail(e);                         \
+  }                                                    \
+  catch (const ::zrt::Error& e) {                      \
+    return ::zrt::fail(e.code, e.what());              \
+  }                                                    \
+  catch (const std::bad_alloc&) {                      \
+    return ::zrt::fail(ZRT_E_NOMEM, "OutOfMemory");    \
+  }
+
+constexpr const char* kOverflowMsg = "BVH traversal stack overflow (tree deeper than the stack was sized for)";
+
+// The device error flag of the context's last launch, copied to pinned host
+// memory behind ev_done.  wait: block until the launch is done and report its
+// error (every such call does); else (render_tiles' sticky check) report it only
+// if the launch has finished and no call has reported it yet.
+int launch_status(zrt_ctx* c, bool wait) {
+  if (!c->launched) return ZRT_OK;
+  if (wait) {
+    HIPCHK(hipEventSynchronize(c->ev_done));
+  } else if (hipEventQuery(c->ev_done) != hipSuccess || c->err_reported) {
+    return ZRT_OK;
+  }
+  if (*c->err_host == 0) return ZRT_OK;
+  c->err_reported = true;
+  return fail(ZRT_E_UNSUPPORTED, kOverflowMsg);
 }
 
 // RCCL for zrt_render_multi, opened on first use so that single-GPU callers do
@@ -1792,10 +1850,15 @@ std::unique_ptr<zrt_ctx> ctx_on_device(const HostScene& h, int device) {
   std::unique_ptr<zrt_ctx> c(new zrt_ctx);
   c->device = device;
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // a blocking stream: work a caller enqueues on the legacy default stream (NULL,
+  // e.g. torch's default stream) after a render on this one waits for it
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamDefault));
   HIPCHK(hipEventCreate(&c->ev_pre));
   HIPCHK(hipEventCreate(&c->ev0));
   HIPCHK(hipEventCreate(&c->ev1));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->err_host), sizeof(unsigned long long), hipHostMallocDefault));
+  *c->err_host = 0;
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, c->device));
   c->cu_count = prop.multiProcessorCount;
@@ -1814,6 +1877,62 @@ struct Comms {
   }
 };
 
+struct CtxDeleter {
+  void operator()(zrt_ctx* c) const { zrt_ctx_destroy(c); }
+};
+
+}  // namespace
+}  // namespace zrt
+
+// One rank per entry of `devices`: its context (scene copy in that GPU's HBM),
+// its padded tile buffer, and - one rank per distinct device - the RCCL
+// communicators, all kept across frames.  Members are destroyed in reverse
+// order: the communicators go before the contexts.
+struct zrt_multi {
+  std::vector<uint32_t> devices;
+  uint32_t n_distinct = 0;
+  bool use_rccl = false;
+  std::vector<std::unique_ptr<zrt_ctx, zrt::CtxDeleter>> ctx;
+  std::vector<zrt::DevBuf<float>> send;
+  zrt::DevBuf<float> gathered, frame;  // on devices[0]
+  zrt::Comms comms;
+};
+
+namespace zrt {
+namespace {
+int assemble(zrt_ctx* c, const zrt_params* p, const float* dev_gathered, uint32_t stride_tiles, float* dev_frame,
+             void* hip_stream) {
+  if (!c || !dev_gathered || !dev_frame) return fail(ZRT_E_INVALID, "null argument");
+  const int rc = validate_params(p);
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    const Geometry g = geometry(p);
+    uint32_t total = 0;
+    if (stride_tiles) {
+      for (uint32_t r = 0; r < p->world_size; ++r)
+        if (rank_tiles(g, r, p->world_size) > stride_tiles)
+          return fail(ZRT_E_INVALID, "stride_tiles is smaller than a rank's tile count");
+      if (uint64_t(stride_tiles) * 64u * p->world_size >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "frame too large");
+      total = stride_tiles * 64u * p->world_size;
+    } else {
+      std::vector<uint32_t> base(p->world_size + 1, 0);
+      for (uint32_t r = 0; r < p->world_size; ++r) base[r + 1] = base[r] + rank_tiles(g, r, p->world_size) * 64u;
+      c->rank_base.upload(base);
+      total = base[p->world_size];
+    }
+    HIPCHK(hipMemsetAsync(dev_frame, 0, sizeof(float) * 3 * size_t(p->width) * p->height, st));
+    if (total) {
+      hipLaunchKernelGGL(assemble_kernel, dim3((total + 255) / 256), dim3(256), 0, st, dev_gathered, dev_frame,
+                         stride_tiles ? nullptr : c->rank_base.p, p->world_size, g.tiles_x, g.xbound, p->height,
+                         p->width, total, stride_tiles * 64u, g.n_tiles);
+      HIPCHK(hipGetLastError());
+    }
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
 }  // namespace
 }  // namespace zrt
 
@@ -1873,8 +1992,18 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
   if (!c || !cam || !dev_tiles) return fail(ZRT_E_INVALID, "null argument");
   int rc = zrt::validate_params(p);
   if (rc) return rc;
+  if (int(p->device) != c->device)
+    return fail(ZRT_E_INVALID, "params->device differs from the device the context was created on");
+  if ((p->bounded_volume_hierarchy != 0 && c->n_prims > 10) != c->use_bvh)
+    return fail(ZRT_E_INVALID,
+                "params->bounded_volume_hierarchy implies another preprocessSufraces decision (raytrace.zig:124-133) "
+                "than the one the context was built with");
   try {
     HIPCHK(hipSetDevice(c->device));
+    // a device error of the previous launch that finished meanwhile is reported
+    // here (sticky), so a caller that never synchronises through the ABI still sees it
+    rc = zrt::launch_status(c, false);
+    if (rc) return rc;
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     const zrt::Geometry g = zrt::geometry(p);
     const uint32_t my_tiles = zrt::rank_tiles(g, p->rank, p->world_size);
@@ -1886,7 +2015,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // LDS budget (else the 32-bit flavour, whose deep rows go to global memory)
     const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
     // (FAST also holds the reference traversal's rows for its order-hazard replay)
-    const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
+    uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
+    if (const char* cap = std::getenv("ZRT_DEBUG_STACK_CAP"))  // tests: a stack too small for the tree
+      stack_depth = std::max<uint32_t>(4, std::min<uint32_t>(stack_depth, uint32_t(std::atoi(cap))));
     const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
                                        size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
                                  : c->n_nodes < 65536;
@@ -1956,7 +2087,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.total_work = work;
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.stack_depth = stack_depth;
-    a.ref_stack = c->stack_depth;
+    a.ref_stack = std::min(c->stack_depth, stack_depth);
     a.leaf_of_slot = c->leaf_of_slot.p;
     a.wnodes = c->wnodes.p;
     a.wide_stride = c->wide_stride;
@@ -1993,9 +2124,13 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       const uint32_t n_slots = my_tiles * 64u;
       hipLaunchKernelGGL(zrt::finalize_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st, c->partial.p,
                          dev_tiles, n_slots, n_chunks, p->world_size, p->rank, g.tiles_x, g.xbound, p->height,
-                         a.color_scale);
+                         a.color_scale, c->scratch.p + zrt::kErrorSlot);
       HIPCHK(hipGetLastError());
     }
+    HIPCHK(hipMemcpyAsync(c->err_host, c->scratch.p + zrt::kErrorSlot, sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(c->ev_done, st));
+    c->err_reported = false;
     // count the pixels this rank renders (for samples/pixels counters)
     uint64_t pixels = 0;
     for (uint32_t lt = 0; lt < my_tiles; ++lt) {
@@ -2010,9 +2145,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_mode = mode;
     c->launched = 1;
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
@@ -2020,8 +2154,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
   if (!c->launched) return fail(ZRT_E_INVALID, "zrt_ctx_stats before any zrt_ctx_render_tiles");
   try {
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipEventSynchronize(c->ev1));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventSynchronize(c->ev_done));
     unsigned long long h[zrt::kScratchSlots] = {0};
     HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof(*out));
@@ -2055,11 +2188,18 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->bvh_nodes = c->n_nodes;
     out->bvh_max_depth = c->bvh_depth;
     out->n_gpus = 1;
-    if (h[zrt::kErrorSlot] != 0) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
-    return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
+    return zrt::launch_status(c, true);
   }
+  ZRT_CATCH_ALL
+}
+
+int zrt_ctx_sync(zrt_ctx* c) {
+  if (!c) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    return zrt::launch_status(c, true);
+  }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_debug_counters(zrt_ctx* c, uint64_t* out, uint32_t n) {
@@ -2067,28 +2207,26 @@ int zrt_ctx_debug_counters(zrt_ctx* c, uint64_t* out, uint32_t n) {
   if (!c->launched) return fail(ZRT_E_INVALID, "no kernel launched on this context yet");
   try {
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventSynchronize(c->ev_done));
     unsigned long long h[zrt::kScratchSlots] = {0};
     HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < n && i < uint32_t(zrt::kScratchSlots); ++i) out[i] = h[i];
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_debug_wave_times(zrt_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n_waves) {
   if (!c || !n_waves) return fail(ZRT_E_INVALID, "null argument");
   try {
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->launched) HIPCHK(hipEventSynchronize(c->ev_done));
     *n_waves = ZRT_PROFILE ? c->n_waves : 0u;
     const size_t n = std::min<size_t>(cap / 2, *n_waves);
     if (n && out) HIPCHK(hipMemcpy(out, c->wave_times.p, 2 * n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_debug_schedule(zrt_ctx* c, uint32_t* costs, uint32_t* order, uint32_t cap, uint32_t* n_tiles) {
@@ -2096,15 +2234,14 @@ int zrt_ctx_debug_schedule(zrt_ctx* c, uint32_t* costs, uint32_t* order, uint32_
   if (!c->launched) return fail(ZRT_E_INVALID, "no kernel launched on this context yet");
   try {
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventSynchronize(c->ev_done));
     *n_tiles = c->scheduled ? c->tile_ids_n : 0u;
     const size_t n = std::min<size_t>(cap, *n_tiles);
     if (n && costs) HIPCHK(hipMemcpy(costs, c->tile_cost.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (n && order) HIPCHK(hipMemcpy(order, c->tile_order.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_last_kernel_ms(zrt_ctx* c, double* ms) {
@@ -2116,36 +2253,20 @@ int zrt_ctx_last_kernel_ms(zrt_ctx* c, double* ms) {
     float f = 0.0f;
     HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
     *ms = f;
-    return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
+    return zrt::launch_status(c, true);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_ctx_assemble(zrt_ctx* c, const zrt_params* p, const float* dev_gathered, float* dev_frame,
                      void* hip_stream) {
-  if (!c || !dev_gathered || !dev_frame) return fail(ZRT_E_INVALID, "null argument");
-  const int rc = zrt::validate_params(p);
-  if (rc) return rc;
-  try {
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    const zrt::Geometry g = zrt::geometry(p);
-    std::vector<uint32_t> base(p->world_size + 1, 0);
-    for (uint32_t r = 0; r < p->world_size; ++r) base[r + 1] = base[r] + zrt::rank_tiles(g, r, p->world_size) * 64u;
-    c->rank_base.upload(base);
-    const uint32_t total = base[p->world_size];
-    HIPCHK(hipMemsetAsync(dev_frame, 0, sizeof(float) * 3 * size_t(p->width) * p->height, st));
-    if (total) {
-      hipLaunchKernelGGL(zrt::assemble_kernel, dim3((total + 255) / 256), dim3(256), 0, st, dev_gathered,
-                         dev_frame, c->rank_base.p, p->world_size, g.tiles_x, g.xbound, p->height, p->width,
-                         total);
-      HIPCHK(hipGetLastError());
-    }
-    return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
-  }
+  return zrt::assemble(c, p, dev_gathered, 0, dev_frame, hip_stream);
+}
+
+int zrt_ctx_assemble_padded(zrt_ctx* c, const zrt_params* p, const float* dev_gathered, uint32_t stride_tiles,
+                            float* dev_frame, void* hip_stream) {
+  if (stride_tiles == 0) return fail(ZRT_E_INVALID, "stride_tiles must be > 0");
+  return zrt::assemble(c, p, dev_gathered, stride_tiles, dev_frame, hip_stream);
 }
 
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
@@ -2178,141 +2299,178 @@ int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_param
     if (rc) return rc;
     if (stats) *stats = s;
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
-int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
-                     const uint32_t* devices, uint32_t n_devices, float* out_rgb, zrt_stats* stats) {
-  if (!camera || !out_rgb || !devices) return fail(ZRT_E_INVALID, "null argument");
+// ---- several GPUs from one host thread (zrt_multi_*, zrt_render_multi) -------
+int zrt_multi_create(const zrt_scene* scene, const zrt_params* params, const uint32_t* devices,
+                     uint32_t n_devices, zrt_multi** out) {
+  if (!out || !devices) return fail(ZRT_E_INVALID, "null argument");
+  *out = nullptr;
   if (n_devices == 0 || n_devices > 1024) return fail(ZRT_E_INVALID, "n_devices must be in 1..1024");
-  int rc = zrt::validate_params(params);
-  if (rc) return rc;
-  rc = zrt::validate_scene(scene);
+  if (!params) return fail(ZRT_E_INVALID, "params is null");
+  int rc = zrt::validate_scene(scene);
   if (rc) return rc;
   for (uint32_t r = 0; r < n_devices; ++r) {
     rc = zrt::check_device(int(devices[r]));
     if (rc) return rc;
   }
-  std::vector<uint32_t> distinct(devices, devices + n_devices);
-  std::sort(distinct.begin(), distinct.end());
-  distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
-  const bool one_rank_per_device = distinct.size() == n_devices;
-  using CtxPtr = std::unique_ptr<zrt_ctx, int (*)(zrt_ctx*)>;
-  std::vector<CtxPtr> ctx;
-  std::vector<zrt_params> rp(n_devices, *params);
+  try {
+    std::unique_ptr<zrt_multi> m(new zrt_multi);
+    m->devices.assign(devices, devices + n_devices);
+    std::vector<uint32_t> distinct(m->devices);
+    std::sort(distinct.begin(), distinct.end());
+    distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+    m->n_distinct = uint32_t(distinct.size());
+    // RCCL only where there is something to move between GPUs: one rank per
+    // device, at least two devices (a device listed twice gathers by copies)
+    m->use_rccl = m->n_distinct == n_devices && n_devices > 1;
+    // the scene flattened once (BVH build, raytrace.zig:124-133), a copy on every GPU
+    const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
+    zrt::HostScene host;
+    zrt::flatten_scene(&host, scene, use_bvh);
+    for (uint32_t r = 0; r < n_devices; ++r) m->ctx.emplace_back(zrt::ctx_on_device(host, int(devices[r])).release());
+    m->send.resize(n_devices);
+    if (m->use_rccl) {
+      // communicators live as long as the context (not per frame)
+      const zrt::Rccl& R = zrt::rccl();
+      m->comms.R = &R;
+      m->comms.c.assign(n_devices, nullptr);
+      std::vector<int> devs(devices, devices + n_devices);
+      NCCLCHK(R, R.comm_init_all(m->comms.c.data(), int(n_devices), devs.data()));
+    }
+    *out = m.release();
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_multi_destroy(zrt_multi* m) {
+  if (!m) return ZRT_OK;
+  for (auto& c : m->ctx) {
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+  }
+  delete m;
+  return ZRT_OK;
+}
+
+int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* params, float* out_rgb,
+                     zrt_stats* stats) {
+  if (!m || !camera || !out_rgb) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::validate_params(params);
+  if (rc) return rc;
+  const uint32_t n = uint32_t(m->ctx.size());
   try {
     const zrt::Geometry g = zrt::geometry(params);
-    std::vector<uint32_t> count(n_devices), base(n_devices + 1, 0);
+    std::vector<zrt_params> rp(n, *params);
+    std::vector<uint32_t> count(n), base(n + 1, 0);
     uint32_t max_tiles = 0;
-    for (uint32_t r = 0; r < n_devices; ++r) {
+    for (uint32_t r = 0; r < n; ++r) {
       rp[r].rank = r;
-      rp[r].world_size = n_devices;
-      rp[r].device = devices[r];
-      count[r] = zrt::rank_tiles(g, r, n_devices);
+      rp[r].world_size = n;
+      rp[r].device = m->devices[r];
+      count[r] = zrt::rank_tiles(g, r, n);
       base[r + 1] = base[r] + count[r];
       max_tiles = std::max(max_tiles, count[r]);
     }
     const size_t slot = 64 * 3;  // floats per tile
-    // the scene flattened once (BVH build, raytrace.zig:124-133), then every GPU
-    // gets its own copy and a tile buffer padded to the largest rank's
-    // (ncclGather sends equal counts)
-    const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
-    zrt::HostScene host;
-    zrt::flatten_scene(&host, scene, use_bvh);
-    std::vector<zrt::DevBuf<float>> send(n_devices);
-    for (uint32_t r = 0; r < n_devices; ++r) {
-      zrt_ctx* c = zrt::ctx_on_device(host, int(devices[r])).release();
-      ctx.emplace_back(c, zrt_ctx_destroy);
-      HIPCHK(hipSetDevice(c->device));
-      send[r].alloc(std::max<size_t>(1, max_tiles * slot));
+    // tile buffers padded to the largest rank's (ncclGather sends equal counts)
+    for (uint32_t r = 0; r < n; ++r) {
+      HIPCHK(hipSetDevice(m->ctx[r]->device));
+      if (m->send[r].n < std::max<size_t>(1, max_tiles * slot)) m->send[r].alloc(std::max<size_t>(1, max_tiles * slot));
     }
     // the sampling loops, all enqueued before any is waited on
-    for (uint32_t r = 0; r < n_devices; ++r) {
-      rc = zrt_ctx_render_tiles(ctx[r].get(), camera, &rp[r], send[r].p, nullptr);
+    for (uint32_t r = 0; r < n; ++r) {
+      rc = zrt_ctx_render_tiles(m->ctx[r].get(), camera, &rp[r], m->send[r].p, nullptr);
       if (rc) return rc;
     }
     zrt_stats sum;
     std::memset(&sum, 0, sizeof(sum));
-    for (uint32_t r = 0; r < n_devices; ++r) {
+    int device_rc = ZRT_OK;
+    for (uint32_t r = 0; r < n; ++r) {
       zrt_stats s;
-      rc = zrt_ctx_stats(ctx[r].get(), &s);  // waits for rank r's stream
-      if (rc) return rc;
-      if (r == 0) sum = s;
-      else {
-        sum.recursion_depth_hits += s.recursion_depth_hits;
-        sum.reflections += s.reflections;
-        sum.background_hits += s.background_hits;
-        sum.pixels_processed += s.pixels_processed;
-        sum.samples_processed += s.samples_processed;
-        sum.rays_processed += s.rays_processed;
-        sum.node_visits += s.node_visits;
-        sum.prim_tests += s.prim_tests;
-        sum.sphere_tests += s.sphere_tests;
-        sum.shade_fetches += s.shade_fetches;
-        sum.texel_fetches += s.texel_fetches;
-        sum.leaf_visits += s.leaf_visits;
-        sum.preprocess_ms = std::max(sum.preprocess_ms, s.preprocess_ms);
-        sum.upload_ms = std::max(sum.upload_ms, s.upload_ms);
-        sum.render_ms = std::max(sum.render_ms, s.render_ms);
-        sum.schedule_ms = std::max(sum.schedule_ms, s.schedule_ms);
+      rc = zrt_ctx_stats(m->ctx[r].get(), &s);  // waits for rank r's launch
+      if (rc == ZRT_E_UNSUPPORTED) device_rc = rc;  // device error: finish the frame (NaN tiles), then report it
+      else if (rc) return rc;
+      if (r == 0) {
+        sum = s;
+        continue;
       }
+      sum.recursion_depth_hits += s.recursion_depth_hits;
+      sum.reflections += s.reflections;
+      sum.background_hits += s.background_hits;
+      sum.pixels_processed += s.pixels_processed;
+      sum.samples_processed += s.samples_processed;
+      sum.rays_processed += s.rays_processed;
+      sum.node_visits += s.node_visits;
+      sum.prim_tests += s.prim_tests;
+      sum.sphere_tests += s.sphere_tests;
+      sum.shade_fetches += s.shade_fetches;
+      sum.texel_fetches += s.texel_fetches;
+      sum.leaf_visits += s.leaf_visits;
+      sum.order_replays += s.order_replays;
+      sum.preprocess_ms = std::max(sum.preprocess_ms, s.preprocess_ms);
+      sum.upload_ms = std::max(sum.upload_ms, s.upload_ms);
+      sum.render_ms = std::max(sum.render_ms, s.render_ms);
+      sum.schedule_ms = std::max(sum.schedule_ms, s.schedule_ms);
     }
-    // the gather to devices[0], then the rank-major un-padded order zrt_ctx_assemble reads
+    // the gather to devices[0] in the padded rank-major layout (rank r at
+    // r * max_tiles tiles), which zrt_ctx_assemble_padded reads as it lies
     const double t0 = zrt::now_ms();
-    zrt_ctx* root = ctx[0].get();
+    zrt_ctx* root = m->ctx[0].get();
     HIPCHK(hipSetDevice(root->device));
-    zrt::DevBuf<float> gathered, packed, frame;
-    packed.alloc(std::max<size_t>(1, size_t(base[n_devices]) * slot));
-    frame.alloc(size_t(params->width) * params->height * 3);
-    if (one_rank_per_device) {
-      const zrt::Rccl& R = zrt::rccl();
-      gathered.alloc(std::max<size_t>(1, size_t(n_devices) * max_tiles * slot));
-      zrt::Comms comms;
-      comms.R = &R;
-      comms.c.assign(n_devices, nullptr);
-      std::vector<int> devs(devices, devices + n_devices);
-      NCCLCHK(R, R.comm_init_all(comms.c.data(), int(n_devices), devs.data()));
+    const size_t frame_n = size_t(params->width) * params->height * 3;
+    if (m->frame.n < frame_n) m->frame.alloc(frame_n);
+    const size_t gathered_n = std::max<size_t>(1, size_t(n) * max_tiles * slot);
+    if (m->gathered.n < gathered_n) m->gathered.alloc(gathered_n);
+    if (m->use_rccl) {
+      const zrt::Rccl& R = *m->comms.R;
       NCCLCHK(R, R.group_start());
-      for (uint32_t r = 0; r < n_devices; ++r)
-        NCCLCHK(R, R.gather(send[r].p, r == 0 ? gathered.p : nullptr, size_t(max_tiles) * slot, ncclFloat32, 0,
-                            comms.c[r], ctx[r]->stream));
+      for (uint32_t r = 0; r < n; ++r)
+        NCCLCHK(R, R.gather(m->send[r].p, r == 0 ? m->gathered.p : nullptr, size_t(max_tiles) * slot, ncclFloat32, 0,
+                            m->comms.c[r], m->ctx[r]->stream));
       NCCLCHK(R, R.group_end());
-      HIPCHK(hipSetDevice(root->device));
-      for (uint32_t r = 0; r < n_devices; ++r)
-        if (count[r])
-          HIPCHK(hipMemcpyAsync(packed.p + size_t(base[r]) * slot, gathered.p + size_t(r) * max_tiles * slot,
-                                size_t(count[r]) * slot * sizeof(float), hipMemcpyDeviceToDevice, root->stream));
-      // every rank's gather must be done before the communicators and the send
-      // buffers go
-      for (uint32_t r = 0; r < n_devices; ++r) {
-        HIPCHK(hipSetDevice(ctx[r]->device));
-        HIPCHK(hipStreamSynchronize(ctx[r]->stream));
+      // every rank's part of the gather is done before the next frame reuses its buffer
+      for (uint32_t r = 1; r < n; ++r) {
+        HIPCHK(hipSetDevice(m->ctx[r]->device));
+        HIPCHK(hipStreamSynchronize(m->ctx[r]->stream));
       }
       HIPCHK(hipSetDevice(root->device));
     } else {
-      for (uint32_t r = 0; r < n_devices; ++r)
+      // one device (or ranks sharing devices): copies; every rank's launch is done (stats above)
+      for (uint32_t r = 0; r < n; ++r)
         if (count[r])
-          HIPCHK(hipMemcpyPeerAsync(packed.p + size_t(base[r]) * slot, root->device, send[r].p, ctx[r]->device,
-                                    size_t(count[r]) * slot * sizeof(float), root->stream));
+          HIPCHK(hipMemcpyPeerAsync(m->gathered.p + size_t(r) * max_tiles * slot, root->device, m->send[r].p,
+                                    m->ctx[r]->device, size_t(count[r]) * slot * sizeof(float), root->stream));
     }
-    rc = zrt_ctx_assemble(root, &rp[0], packed.p, frame.p, nullptr);
+    rc = zrt_ctx_assemble_padded(root, &rp[0], m->gathered.p, std::max(1u, max_tiles), m->frame.p, nullptr);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(root->stream));
     sum.gather_ms = zrt::now_ms() - t0;
-    HIPCHK(hipMemcpy(out_rgb, frame.p, sizeof(float) * 3 * size_t(params->width) * params->height,
-                     hipMemcpyDeviceToHost));
-    sum.n_gpus = uint32_t(distinct.size());
+    HIPCHK(hipMemcpy(out_rgb, m->frame.p, sizeof(float) * frame_n, hipMemcpyDeviceToHost));
+    sum.n_gpus = m->n_distinct;
     if (stats) *stats = sum;
+    if (device_rc) return fail(device_rc, zrt::kOverflowMsg);
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
-  } catch (const zrt::Error& e) {
-    return fail(e.code, e.what());
-  } catch (const std::bad_alloc&) {
-    return fail(ZRT_E_NOMEM, "OutOfMemory");
   }
+  ZRT_CATCH_ALL
+}
+
+int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
+                     const uint32_t* devices, uint32_t n_devices, float* out_rgb, zrt_stats* stats) {
+  if (!camera || !out_rgb || !devices) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::validate_params(params);
+  if (rc) return rc;
+  zrt_multi* m = nullptr;
+  rc = zrt_multi_create(scene, params, devices, n_devices, &m);
+  if (rc) return rc;
+  rc = zrt_multi_render(m, camera, params, out_rgb, stats);
+  const std::string msg = zrt_last_error();
+  zrt_multi_destroy(m);
+  if (rc) return fail(rc, msg);
+  return ZRT_OK;
 }
 
 int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* rays, uint32_t n_rays, float* out_t,
@@ -2420,9 +2578,8 @@ int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t 
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, dout.p, n * sizeof(float), hipMemcpyDeviceToHost));
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device) {
@@ -2441,9 +2598,8 @@ int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, d.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ZRT_OK;
-  } catch (const zrt::HipError& e) {
-    return zrt::hip_fail(e);
   }
+  ZRT_CATCH_ALL
 }
 
 }  // extern "C"

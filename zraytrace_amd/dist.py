@@ -3,8 +3,9 @@
 8x8 tiles are dealt round-robin (tile t -> rank t % world, zrt.h); each rank
 renders its tiles into a buffer padded to the largest rank's size, and one
 gather to the destination rank (RCCL over xGMI with the "nccl" backend; gloo
-in the CPU tests) collects them.  The gathered, un-padded buffer is rank-major,
-which is what zrt_ctx_assemble expects.
+in the CPU tests) collects them straight into one padded, rank-major buffer
+(rank r at tile r * max_tiles), which zrt_ctx_assemble_padded reads as it
+lies: no un-padding copy.
 """
 from __future__ import annotations
 
@@ -26,18 +27,93 @@ def tile_counts(params) -> list:
     return out
 
 
-def gather_tiles(tiles, counts, rank, world, dst=0, group=None):
-    """Gather every rank's padded tile buffer to `dst`; returns the rank-major,
-    un-padded concatenation on `dst` and None elsewhere."""
+def gather_tiles(tiles, counts, rank, world, dst=0, group=None, out=None):
+    """Gather every rank's padded tile buffer (max(counts) tiles) to `dst`.
+
+    Returns, on `dst`, the padded rank-major buffer: rank r's tiles at
+    r * max(counts) * 64 * 3 floats (`out` if given, on the device of `tiles`);
+    None on the other ranks.  With the nccl backend the per-rank receive
+    buffers are views into that one buffer, so RCCL writes each rank's tiles
+    in place; gloo (CPU rehearsal, ranks may share a GPU) gathers host copies
+    and moves the whole buffer to the device once."""
     import torch
     import torch.distributed as dist
+    per_rank = max(counts) * 64 * 3
+    if tiles.numel() < per_rank:
+        raise ValueError(f"tile buffer holds {tiles.numel()} floats, the padded gather needs {per_rank}")
+    send = tiles[:per_rank]
     if world == 1:
-        return tiles[: counts[0] * 64 * 3]
-    send = tiles
-    if tiles.is_cuda and dist.get_backend(group) == "gloo":
-        send = tiles.cpu()  # gloo gathers host tensors (multi-rank rehearsal on one GPU)
-    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+        if out is not None:
+            out[:per_rank].copy_(send)
+            return out
+        return send
+    gloo = dist.get_backend(group) == "gloo"
+    if gloo and send.is_cuda:
+        send = send.cpu()  # gloo gathers host tensors
+    bufs = None
+    if rank == dst:
+        if gloo:
+            host = torch.empty(world * per_rank, dtype=send.dtype)
+            bufs = [host[r * per_rank:(r + 1) * per_rank] for r in range(world)]
+        else:
+            if out is None:
+                out = torch.empty(world * per_rank, dtype=tiles.dtype, device=tiles.device)
+            bufs = [out[r * per_rank:(r + 1) * per_rank] for r in range(world)]
     dist.gather(send, bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    return torch.cat([b[: c * 64 * 3] for b, c in zip(bufs, counts)]).to(tiles.device)
+    if gloo:
+        if out is None:
+            return host.to(tiles.device)
+        out[: world * per_rank].copy_(host)
+    return out
+
+
+class TileFrame:
+    """One frame of the tile partition on this rank, as bench.py times it:
+    render this rank's tiles (scene resident in HBM), gather all ranks' tiles
+    to rank 0 (RCCL over xGMI, or gloo), assemble the framebuffer on rank 0.
+
+    Everything is enqueued on one explicit torch stream whose handle is passed
+    to libzrt, so the gather (which torch orders after the current stream) and
+    the assemble see the finalized tiles, with no reliance on libzrt's own
+    stream.  The buffers are allocated once and reused every step."""
+
+    def __init__(self, scene, params, rank: int, world: int):
+        import torch
+        from . import RenderContext, RenderParams
+        self.scene, self.params, self.rank, self.world = scene, params, rank, world
+        self.ctx = RenderContext(scene, params)
+        self.counts = tile_counts(params)
+        self.max_tiles = max(self.counts)
+        dev = torch.device("cuda", params.device)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.tiles = torch.zeros(max(1, self.max_tiles) * 64 * 3, dtype=torch.float32, device=dev)
+        self.gathered = self.frame = None
+        if rank == 0:
+            self.gathered = torch.empty(world * max(1, self.max_tiles) * 64 * 3, dtype=torch.float32, device=dev)
+            self.frame = torch.empty(params.height * params.width * 3, dtype=torch.float32, device=dev)
+        self.p0 = RenderParams(**{**params.__dict__, "rank": 0})
+
+    def step(self, params=None) -> float:
+        """One frame; returns the render launch's kernel time in ms (HIP events
+        on the launch stream).  `params` overrides the render params (e.g. the
+        diagnostic flag) for this step."""
+        import torch
+        p = params or self.params
+        with torch.cuda.stream(self.stream):
+            self.ctx.render_tiles(self.scene.camera, p, self.tiles.data_ptr(), self.stream.cuda_stream)
+            kms = self.ctx.kernel_ms()
+            g = gather_tiles(self.tiles, self.counts, self.rank, self.world, dst=0, out=self.gathered)
+            if self.rank == 0:
+                self.ctx.assemble_padded(self.p0, g.data_ptr(), max(1, self.max_tiles), self.frame.data_ptr(),
+                                         self.stream.cuda_stream)
+        return kms
+
+    def image(self):
+        """Rank 0: the assembled framebuffer as numpy [H, W, 3] (row 0 = bottom)."""
+        self.stream.synchronize()
+        return self.frame.cpu().numpy().reshape(self.params.height, self.params.width, 3)
+
+    def close(self):
+        self.ctx.close()
