@@ -14,10 +14,12 @@ value = rays of all ranks (raytrace.zig:69's rays_processed, counted on the
 device) / the max-over-ranks wall time of the timed steps, in Mrays/s.
 
 roofline: the render kernel's position against every ceiling it could be
-bound by - VALU issue, L1 (TCP) accesses, L2 -> L1 lines, HBM - each
-"achieved" = a per-launch PMC count (rocprofv3 passes of this exact config,
-profiles/latest_pmc.json) / the launch's HIP-event time measured in this run;
-"bound" is the ceiling with the largest fraction.
+bound by - TD (vector-memory data return) busy, VALU issue, L1 (TCP)
+accesses, L1 -> L2 requests, HBM - each "achieved" = a per-launch PMC count
+(rocprofv3 passes of this exact config, profiles/latest_pmc.json) / the
+launch's HIP-event time measured in this run, against per-clock peaks measured
+by tools/ubench.hip (profiles/ubench.json); "bound" is the ceiling with the
+largest fraction.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -40,12 +42,8 @@ SCENES = {0: "manAndBall: models/Man_LOD3.obj + ground sphere", 1: "threeBalls: 
           6: "texturedTeapot: the C5 substitute, 1.6 M subdivided teapot triangles + image textures"}
 # 0-5: scenes.zig:267-277; 6: DESIGN.md section 4
 
-# Ceilings.  Spec / guide values (MI355X_MICROARCH.md), replaced by the measured
-# ones of tools/ubench.hip when profiles/ubench.json holds them.
-HBM_PEAK_GBS = 8000.0  # HBM3E spec (chip-level parameters)
-# 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles x 2.4 GHz
-VALU_ISSUE_PEAK = 256 * 4 * 2400e6 / 2
-L2_PEAK_GBS = 34500.0  # L2 aggregate (guide §L2)
+HBM_PEAK_GBS = 8000.0  # HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
 def log(*a):
@@ -78,51 +76,52 @@ def pmc_entry(config):
     return None
 
 
-def ceilings():
-    """Peak rates: measured by tools/ubench.hip on the GPU box (profiles/ubench.json) where present."""
-    c = {"valu_issue": {"peak": VALU_ISSUE_PEAK, "unit": "wave64 VALU inst/s", "source": "guide: 1024 SIMD-32 x 1/2 cyc x 2.4 GHz"},
-         "l1_access": None, "l2_lines": None,
-         "hbm": {"peak": HBM_PEAK_GBS * 1e9, "unit": "B/s", "source": "HBM3E spec (guide)"}}
+def ubench_peaks():
+    """Per-clock ceilings measured by tools/ubench.hip under rocprofv3 on the GPU box
+    (profiles/ubench.json, tools/gpu_ubench.sh); the guide's figures where absent."""
     try:
         with open(os.path.join(REPO, "profiles", "ubench.json")) as f:
-            u = json.load(f)
-    except (OSError, ValueError):
-        u = {}
-    if u.get("valu_insts_per_s"):
-        c["valu_issue"] = {"peak": u["valu_insts_per_s"], "unit": "wave64 VALU inst/s",
-                           "source": "profiles/ubench.json (tools/ubench.hip valu_kernel, SQ_INSTS_VALU / time)"}
-    if u.get("tcp_accesses_per_s"):
-        c["l1_access"] = {"peak": u["tcp_accesses_per_s"], "unit": "TCP accesses/s",
-                          "source": "profiles/ubench.json (tools/ubench.hip load_kernel, TCP_TOTAL_CACHE_ACCESSES / time)"}
-    if u.get("tcp_tcc_read_req_per_s"):
-        c["l2_lines"] = {"peak": u["tcp_tcc_read_req_per_s"], "unit": "L1->L2 read requests/s",
-                         "source": "profiles/ubench.json (tools/ubench.hip l2 load kernel, TCP_TCC_READ_REQ / time)"}
-    else:
-        c["l2_lines"] = {"peak": L2_PEAK_GBS * 1e9 / 128, "unit": "L1->L2 read requests/s",
-                         "source": "guide L2 34.5 TB/s / 128-B lines"}
-    return c
+            return json.load(f)["peaks_per_clock"], "profiles/ubench.json (tools/ubench.hip, rocprofv3 --pmc)"
+    except (OSError, ValueError, KeyError):
+        return ({"valu_insts_per_simd": 0.5, "tcp_accesses_per_cu": 1.0, "l2_read_req_per_cu": 0.375},
+                "MI355X_MICROARCH.md (one wave64 VALU per 2 cycles per SIMD; 64 B/clk/CU L1; L2 34.5 TB/s)")
 
 
 def roofline(pmc, kernel_s, algo_bytes, diag):
-    """Every ceiling's fraction for the launch: PMC counts per launch / the live
-    HIP-event launch time; bound = the largest fraction."""
+    """The render launch against every ceiling it could be bound by.  Per ceiling:
+    the PMC count per launch (rocprofv3 pass of this exact config) / the launch's
+    HIP-event time measured in this run = achieved, against the measured per-clock
+    peak x the clock the PMC pass saw (GRBM_GUI_ACTIVE per XCD / its duration):
+      vmem_td     TD (vector-memory data return) busy cycles per CU; peak = every cycle
+      valu_issue  wave64 VALU instructions; peak = the 2-source class issue rate
+      l1_access   TCP (L1) cache accesses; peak = the best load pattern's rate
+      l2_lines    L1 -> L2 read requests; peak = an all-miss L1 pattern's rate
+      hbm         (2 FETCH_SIZE + WRITE_SIZE) KiB; peak = 8 TB/s
+    bound = the ceiling with the largest fraction."""
     out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
            "kernel_s": round(kernel_s, 6)}
-    cs = ceilings()
     rows = {}
     if pmc:
-        sq = pmc.get("sq") or {}
-        cache = pmc.get("cache") or {}
-        meas = {"valu_issue": sq.get("SQ_INSTS_VALU"),
-                "l1_access": cache.get("TCP_TOTAL_CACHE_ACCESSES_sum"),
-                "l2_lines": cache.get("TCP_TCC_READ_REQ_sum"),
-                "hbm": pmc.get("hbm_bytes_per_launch")}
-        for k, per_launch in meas.items():
-            if per_launch is None or cs.get(k) is None:
+        peaks, src = ubench_peaks()
+        sq, cache = pmc.get("sq") or {}, pmc.get("cache") or {}
+        dur = min(pmc["duration_ns_per_pass"]) * 1e-9
+        clk = cache["GRBM_GUI_ACTIVE"] / N_XCD / dur if cache.get("GRBM_GUI_ACTIVE") else 2.4e9
+        out["clock_ghz"] = round(clk / 1e9, 3)
+        spec = {"vmem_td": (cache.get("TD_TD_BUSY_sum", 0) / N_CU or None, clk, "TD busy cycles/s per CU"),
+                "valu_issue": (sq.get("SQ_INSTS_VALU"), peaks["valu_insts_per_simd"] * N_SIMD * clk,
+                               "wave64 VALU inst/s"),
+                "l1_access": (cache.get("TCP_TOTAL_CACHE_ACCESSES_sum"), peaks["tcp_accesses_per_cu"] * N_CU * clk,
+                              "TCP accesses/s"),
+                "l2_lines": (cache.get("TCP_TCC_READ_REQ_sum"), peaks["l2_read_req_per_cu"] * N_CU * clk,
+                             "L1->L2 read requests/s"),
+                "hbm": (pmc.get("hbm_bytes_per_launch"), HBM_PEAK_GBS * 1e9, "B/s")}
+        for k, (per_launch, peak, unit) in spec.items():
+            if not per_launch:
                 continue
             a = per_launch / kernel_s
-            rows[k] = {"per_launch": per_launch, "achieved": a, "peak": cs[k]["peak"], "unit": cs[k]["unit"],
-                       "frac": round(a / cs[k]["peak"], 4), "peak_source": cs[k]["source"]}
+            rows[k] = {"per_launch": per_launch, "achieved": float(f"{a:.4e}"), "peak": float(f"{peak:.4e}"),
+                       "unit": unit, "frac": round(a / peak, 4)}
+        out["peak_source"] = src
         out["traffic"] = pmc.get("hbm_bytes_per_launch")
         out["pmc_source"] = pmc.get("source")
         out["valu_lane_util"] = sq.get("valu_lane_util")
@@ -139,7 +138,7 @@ def roofline(pmc, kernel_s, algo_bytes, diag):
     rays = max(1, diag["rays_processed"])
     out["algorithmic"] = {
         "bytes_per_launch": int(algo_bytes), "gbs": round(algo_bytes / kernel_s / 1e9, 1),
-        "note": "bytes each ray's node/primitive/material reads and path-state writes touch; served by L1/L2 "
+        "note": "bytes each ray's node/primitive/material reads and path-state writes touch; served by LDS/L1/L2 "
                 "(the bunny scene is ~2 MB), so this is not an HBM figure and carries no HBM fraction",
         "per_ray": {"node_visits": round(diag["node_visits"] / rays, 2),
                     "leaf_visits": round(diag["leaf_visits"] / rays, 2),

@@ -24,8 +24,8 @@
 
 constexpr int kIters = 4096;
 
-// 8 independent f32 multiply-add chains (separate v_mul / v_add, no FMA):
-// 16 VALU per iteration, no memory traffic.
+// 8 independent f32 multiply-add chains (the compiler fuses each into one
+// v_fma_f32): 8 VALU per iteration, no memory traffic.
 __global__ void __launch_bounds__(256) valu_kernel(float* out, float a, float b) {
   float x[8];
 #pragma unroll
@@ -39,6 +39,30 @@ __global__ void __launch_bounds__(256) valu_kernel(float* out, float a, float b)
   for (int k = 0; k < 8; ++k) s += x[k];
   if (s == 12345.678f) out[blockIdx.x] = s;  // keep the chains alive
 }
+
+// One VALU instruction class at a time (inline asm, so the compiler neither
+// fuses nor packs): 16 independent chains per wave, 16 instructions per
+// iteration.  Which classes issue at one wave64 instruction per 2 cycles per
+// SIMD and which take longer decides the VALU ceiling of a kernel's mix.
+#define ZRT_UB_VALU(NAME, ASM)                                                               \
+  __global__ void __launch_bounds__(256) NAME(float* out, float a) {                         \
+    float x[16];                                                                            \
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) x[k] = threadIdx.x * 0.001f + k;          \
+    for (int i = 0; i < kIters / 2; ++i) {                                                  \
+      _Pragma("unroll") for (int k = 0; k < 16; ++k) asm volatile(ASM : "+v"(x[k]) : "v"(a)); \
+    }                                                                                       \
+    float s = 0.0f;                                                                         \
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) s += x[k];                               \
+    if (s == 12345.678f) out[blockIdx.x] = s;                                               \
+  }
+ZRT_UB_VALU(valu_add_f32, "v_add_f32 %0, %0, %1")
+ZRT_UB_VALU(valu_mul_f32, "v_mul_f32 %0, %0, %1")
+ZRT_UB_VALU(valu_fma_f32, "v_fma_f32 %0, %0, %1, %1")
+ZRT_UB_VALU(valu_max3_f32, "v_max3_f32 %0, %0, %1, %1")
+ZRT_UB_VALU(valu_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+ZRT_UB_VALU(valu_add_u32, "v_add_u32 %0, %0, %1")
+ZRT_UB_VALU(valu_xor_b32, "v_xor_b32 %0, %0, %1")
+ZRT_UB_VALU(valu_rcp_f32, "v_rcp_f32 %0, %0")
 
 // float4 loads from a table of `mask + 1` float4 (a power of two), index
 // advancing by `step` float4 per lane and per iteration: with a 16 KiB table
@@ -115,9 +139,39 @@ int main() {
     ValuArgs a{grid, out};
     const float ms = time_ms(launch_valu, &a, 5);
     const double waves = double(grid) * 4;
-    const double insts = waves * kIters * 16.0;  // VALU wave-instructions in the loop
+    const double insts = waves * kIters * 8.0;  // VALU wave-instructions in the loop (8 v_fma_f32)
     std::printf(" \"valu\": {\"ms\": %.4f, \"wave_insts\": %.0f, \"wave_insts_per_s\": %.4e},\n", ms, insts,
                 insts / (ms * 1e-3));
+  }
+  {
+    struct {
+      const char* name;
+      void (*fn)(float*, float);
+    } ops[] = {{"add_f32", valu_add_f32}, {"mul_f32", valu_mul_f32}, {"fma_f32", valu_fma_f32},
+               {"max3_f32", valu_max3_f32}, {"cndmask", valu_cndmask}, {"add_u32", valu_add_u32},
+               {"xor_b32", valu_xor_b32}, {"rcp_f32", valu_rcp_f32}};
+    std::printf(" \"valu_ops\": {\n");
+    const int nops = int(sizeof(ops) / sizeof(ops[0]));
+    for (int o = 0; o < nops; ++o) {
+      hipEvent_t e0, e1;
+      CHK(hipEventCreate(&e0));
+      CHK(hipEventCreate(&e1));
+      hipLaunchKernelGGL(ops[o].fn, dim3(grid), dim3(256), 0, 0, out, 0.999f);
+      CHK(hipDeviceSynchronize());
+      CHK(hipEventRecord(e0));
+      for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(ops[o].fn, dim3(grid), dim3(256), 0, 0, out, 0.999f);
+      CHK(hipEventRecord(e1));
+      CHK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double insts = double(grid) * 4 * (kIters / 2) * 16.0;
+      // per SIMD per cycle at the nominal 2.4 GHz (the PMC pass gives the real clock)
+      std::printf("  \"%s\": {\"ms\": %.4f, \"wave_insts_per_s\": %.4e, \"per_simd_per_clk_2400\": %.4f}%s\n",
+                  ops[o].name, ms, insts / (ms * 1e-3), insts / (ms * 1e-3) / (cus * 4.0) / 2.4e9,
+                  o + 1 < nops ? "," : "");
+    }
+    std::printf(" },\n");
   }
   struct Case {
     const char* name;

@@ -157,7 +157,7 @@ void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
 
 }  // namespace
 
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels) {
   WideBvh out;
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
@@ -230,20 +230,36 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves) {
   }
   out.n_nodes = uint32_t(wide.size());
   out.nodes.resize(8 * wide.size());
-  // storage order: depth-first (pre-order, children in slot order), so a
-  // subtree's nodes are adjacent (A/B against the breadth-first construction
-  // order: equal on C4 / C5, +0.7 % on C3)
+  // storage order: the top `top_levels` levels first, breadth-first (render.hip
+  // serves them from LDS: nodes 0 .. n_top-1), then depth-first (pre-order,
+  // children in slot order), so a subtree's nodes are adjacent (A/B against the
+  // breadth-first construction order: equal on C4 / C5, +0.7 % on C3)
   std::vector<int32_t> pos(wide.size(), -1);
   {
-    std::vector<int32_t> todo{0};
     int32_t next_pos = 0;
-    while (!todo.empty()) {
-      const int32_t wi = todo.back();
-      todo.pop_back();
-      pos[size_t(wi)] = next_pos++;
-      for (int k = wide[size_t(wi)].count - 1; k >= 0; --k) {
-        const int32_t c = wide[size_t(wi)].child[k];
-        if (N[c].leaf < 0) todo.push_back(wide_of[c]);
+    std::vector<int32_t> level{0}, roots;  // roots: first nodes below the top levels
+    for (uint32_t l = 0; l < top_levels && !level.empty(); ++l) {
+      std::vector<int32_t> below;
+      for (const int32_t wi : level) {
+        pos[size_t(wi)] = next_pos++;
+        for (int k = 0; k < wide[size_t(wi)].count; ++k) {
+          const int32_t c = wide[size_t(wi)].child[k];
+          if (N[c].leaf < 0) below.push_back(wide_of[c]);
+        }
+      }
+      level.swap(below);
+    }
+    out.n_top = uint32_t(next_pos);
+    for (const int32_t r : level) {
+      std::vector<int32_t> todo{r};
+      while (!todo.empty()) {
+        const int32_t wi = todo.back();
+        todo.pop_back();
+        pos[size_t(wi)] = next_pos++;
+        for (int k = wide[size_t(wi)].count - 1; k >= 0; --k) {
+          const int32_t c = wide[size_t(wi)].child[k];
+          if (N[c].leaf < 0) todo.push_back(wide_of[c]);
+        }
       }
     }
   }

@@ -19,8 +19,10 @@ struct RefLeaf {
 struct WideBvh {
   std::vector<float4v> nodes;   // 8 per wide node, node 0 = root
   uint32_t n_nodes = 0, n_leaves = 0, depth = 0, max_stack = 0;
+  uint32_t n_top = 0;           // nodes of the top levels, stored first (0 .. n_top-1)
 };
 
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves);
+// top_levels: how many levels (root = 1) are stored first, breadth-first.
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels = 2);
 
 }  // namespace zrt

@@ -92,6 +92,13 @@ struct KArgs {
   const uint32_t* __restrict__ leaf_of_slot;  // primitive slot -> its reference BVH leaf node
   void* stack_ovf;       // [row - lds_rows][lane] overflow rows of the FAST stack (StackT)
   unsigned long long seed_mix;
+  // LDS beyond the stack rows (byte offsets into the block's dynamic LDS):
+  uint32_t n_top;         // FAST: wide nodes 0 .. n_top-1 (the top levels) served from LDS
+  uint32_t lds_top_off;   //   [copy][node][8] float4, copied in at kernel start
+  uint32_t lds_att_off;   // attenuation rows 0 .. att_lds_rows-1: [row][rgb][lane] f32
+  uint32_t att_lds_rows;  //   (rows att_lds_rows.. in `att`, [row - att_lds_rows][lane])
+  uint32_t lds_mat_off;   // the material table (n_mats DevMaterial), when mats_in_lds
+  uint32_t n_mats, mats_in_lds;
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -139,6 +146,9 @@ constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #endif
 #if ZRT_HAZARD_ENTRY && !ZRT_OCT_COPIES
 #error "the FAST entry test reads the near planes of the octant copies (ZRT_OCT_COPIES=1)"
+#endif
+#ifndef ZRT_LDS_TOP
+#define ZRT_LDS_TOP 1  // FAST: the wide tree's top levels read from LDS (0: A/B, every node from global memory)
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -625,6 +635,31 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
          (__builtin_fminf(fz, tb) > __builtin_fmaxf(nz, t_min));
 }
 
+constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
+
+// The wide tree's top levels (accel_build.cpp stores them first: nodes 0 ..
+// n_top-1), every octant copy, copied into the block's LDS once at kernel
+// start.  Every ray begins at the root and most go on to a level-1 node, and
+// vector-memory data return (TD) is what the FAST loop saturates:
+// these node reads come from LDS instead.  All threads of the block call this.
+__device__ __forceinline__ void fill_lds_top(const KArgs& a, float4* __restrict__ top) {
+  const uint32_t per = a.n_top * 8u;  // float4 per octant copy
+  for (uint32_t i = threadIdx.x; i < per * kOctCopies; i += kBlock) {
+    const uint32_t o = i / per, j = i - o * per;
+    top[i] = a.wnodes[o * a.wide_stride + j];
+  }
+  __syncthreads();
+}
+
+// The material table (a few records in every reference scene) copied into
+// LDS at kernel start: the shading of a hit reads its material right after its
+// shade record, a dependent chain of loads.
+__device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict__ m) {
+  const float4* src = reinterpret_cast<const float4*>(a.mats);
+  for (uint32_t i = threadIdx.x; i < a.n_mats * 3u; i += kBlock) m[i] = src[i];
+  __syncthreads();
+}
+
 // FAST: near-first over the 4-wide tree (accel_build.cpp), stored once per
 // ray octant with each axis' min / max planes swapped where the octant's
 // direction is negative, so a node's first three float4 are the four slots'
@@ -637,9 +672,9 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
 // farther ones pushed, branch-free.
 template <bool STATS, class StackT>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
-                                              uint32_t gl, float& best_t, int& best, uint32_t& c_nodes,
-                                              uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
-                                              uint32_t& c_replays) {
+                                              const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
+                                              int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
+                                              uint32_t& c_sph, uint32_t& c_replays) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
   // the first rows in LDS, the rest in global memory (32-bit stacks only: the
@@ -666,7 +701,10 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   }
 #endif
   uint32_t sp = 0;
-  const float4* q = a.wnodes + base;  // the root wide node
+  // this octant's copy of the top nodes in LDS; the root is its node 0
+  const float4* __restrict__ top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
+  const uint32_t n_top = ZRT_LDS_TOP ? a.n_top : 0u;
+  const float4* q = ZRT_LDS_TOP ? top : a.wnodes + base;
   float4 nx, ny, nz, fx, fy, fz, ra;
   ZRT_LOAD_NODE(q)
   for (;;) {
@@ -780,8 +818,15 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
 #undef ZRT_WIDE_LEAF
     }
     if (next < 0) break;
-    q = a.wnodes + (base + 8u * (uint32_t)next);
-    ZRT_LOAD_NODE(q)
+    if ((uint32_t)next < n_top) {  // a top-level node: from LDS (ds_read)
+      const float4* __restrict__ t = top + 8u * (uint32_t)next;
+      q = t;
+      ZRT_LOAD_NODE(t)
+    } else {
+      const float4* __restrict__ g = a.wnodes + (base + 8u * (uint32_t)next);
+      q = g;
+      ZRT_LOAD_NODE(g)
+    }
   }
 #undef ZRT_LOAD_NODE
   if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best), 0)) {  // 1e-8..1e-5 of rays
@@ -897,6 +942,15 @@ template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int
 __device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
+  float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  float* att_l = reinterpret_cast<float*>(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
+  const DevMaterial* mats = a.mats;
+  if (a.mats_in_lds) {  // block-uniform
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  }
   const int lane = (int)__lane_id();
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;  // n_lanes < 2^32
 
@@ -1009,7 +1063,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
-        traverse_wide<STATS>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
+        traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
       }
@@ -1023,7 +1077,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         // ---- HitRecord.init (hit_record.zig:28-41)
         const float4 sh = a.shade[best];
         const uint32_t tag = __float_as_uint(sh.w);
-        const MatReg mat = load_material(a.mats, tag & 0x7fffffffu);
+        const MatReg mat = load_material(mats, tag & 0x7fffffffu);
         const uint32_t mkind = mat.kind();
         const bool need_uv = mkind != ZRT_MAT_DIELECTRIC && mat.tex_kind() == ZRT_TEX_IMAGE;
         if (STATS) {
@@ -1098,8 +1152,16 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         } else {
           ++c_refl;
           if (depth_left > 1) {  // an attenuation pushed at depth 1 is never read
-            // every earlier scatter was at a depth > this one, so all were pushed
-            a.att[(uint64_t)(a.max_depth - depth_left) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+            // every earlier scatter was at a depth > this one, so all were pushed;
+            // the first rows live in LDS, deeper ones in global memory
+            const uint32_t i = a.max_depth - depth_left;
+            if (i < a.att_lds_rows) {
+              att_l[(3 * i + 0) * kBlock] = att.x;
+              att_l[(3 * i + 1) * kBlock] = att.y;
+              att_l[(3 * i + 2) * kBlock] = att.z;
+            } else {
+              a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+            }
           }
           o = loc;
           d = nd;
@@ -1116,7 +1178,13 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         // a path that reached the sky traced at depth_left >= 1: all of its
         // max_depth - depth_left scatters were pushed
         for (uint32_t i = a.max_depth - depth_left; i-- > 0;) {
-          const float4 at = a.att[(uint64_t)i * a.n_lanes + gl];
+          V3 at;
+          if (i < a.att_lds_rows) {
+            at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
+          } else {
+            const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
+            at = mk(g.x, g.y, g.z);
+          }
           col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
         }
       }
@@ -1178,6 +1246,8 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
                                                        float* __restrict__ out_t, int32_t* __restrict__ out_slot) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
+  float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
   if (gl >= n) return;
   const float* q = rays + 6ull * gl;
@@ -1196,7 +1266,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
     }
   } else if (MODE == 3) {
     uint32_t c_replays = 0;
-    traverse_wide<false>(a, r, stk, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
+    traverse_wide<false>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
   } else {
     traverse_bvh<MODE == 1, false>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
   }
@@ -1428,7 +1498,7 @@ struct zrt_ctx {
   hipStream_t stream = nullptr;
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0, stack_depth = 0;
-  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0;
+  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0, n_top = 0, n_mats = 0;
   std::vector<uint32_t> slot_to_prim;  // device primitive slot -> reference list index
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
@@ -1479,7 +1549,7 @@ namespace {
 struct HostScene {
   bool use_bvh = false;
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0;
-  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0;
+  uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0, n_top = 0, n_mats = 0;
   uint32_t texel_bytes = 0;
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
@@ -1563,6 +1633,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
     c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
+    c->n_top = wide.n_top;
   } else {
     for (uint32_t i = 0; i < n; ++i) slot_to_prim.push_back(i);
   }
@@ -1695,6 +1766,8 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->stack_depth = h.use_bvh ? h.bvh_depth + 2 : 0;
   c->n_wide = h.n_wide;
   c->n_leaves = h.n_leaves;
+  c->n_top = h.n_top;
+  c->n_mats = uint32_t(h.mats.size());
   c->wide_stack = h.wide_stack;
   c->wide_stride = h.wide_stride;
   c->texel_bytes = h.texel_bytes;
@@ -1725,6 +1798,56 @@ template <int PRNG>
 void* probe_ptr(bool stk16) {
   return stk16 ? reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint16_t>)
                : reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint32_t>);
+}
+
+// The block's dynamic LDS: [stack rows][lane] (StackT), then (FAST) the top
+// wide nodes of every octant copy, then the first attenuation rows
+// [row][rgb][lane] f32.  Sized so the waves per SIMD the kernel is built for
+// (its __launch_bounds__) still fit: 160 KiB / that many blocks per CU.
+struct LdsPlan {
+  uint32_t stack_rows = 0, top_off = 0, att_off = 0, att_rows = 0, mat_off = 0, mats_in_lds = 0;
+  size_t bytes = 0;
+};
+LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth) {
+  const uint32_t waves = mode == 3 ? ZRT_WAVES_WIDE : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
+  // 256-thread blocks: `waves` blocks per CU; 1 KiB below the even share (a
+  // block of exactly 32 KiB ran 8 % slower at 5 blocks per CU)
+  const size_t budget = (160u << 10) / waves - (1u << 10);
+  const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
+  const size_t row_att = 3 * sizeof(float) * kBlock;
+  const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * kOctCopies : 0;
+  // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1)
+  // A/B (C4, interleaved): none 50.35, 1 row 50.57, 2 rows 50.70 Gray/s; 4 rows
+  // (a 32 KiB block, the whole budget) 46.5
+  uint32_t want = 2;
+  if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
+  want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
+  LdsPlan L;
+  if (mode == 3 && !stk16) {
+    // deep trees: the stack takes what the top nodes and two attenuation rows leave
+    want = std::min<uint32_t>(want, 2);
+    const size_t room = budget > top + want * row_att ? budget - top - want * row_att : 0;
+    L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(stack_depth, uint32_t(room / (kBlock * entry))));
+  } else {
+    L.stack_rows = stack_depth;  // the whole stack in LDS (16-bit FAST: it fits kStackLdsBytes)
+  }
+  if (const char* f = std::getenv("ZRT_STACK_LDS_ROWS"))  // tests: force the overflow rows into use
+    if (mode == 3) L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(L.stack_rows, uint32_t(std::atoi(f))));
+  const size_t stack = (size_t(L.stack_rows) * kBlock * entry + 15) & ~size_t(15);
+  const size_t used = stack + top;
+  L.att_rows = std::min<uint32_t>(want, used < budget ? uint32_t((budget - used) / row_att) : 0u);
+  L.top_off = uint32_t(stack);
+  L.att_off = uint32_t(used);
+  L.bytes = used + L.att_rows * row_att;
+  // the material table, if it fits what is left (ZRT_MATS_LDS=0: A/B, always global)
+  const size_t mats = size_t(c->n_mats) * sizeof(DevMaterial);
+  const char* me = std::getenv("ZRT_MATS_LDS");
+  if (mats > 0 && L.bytes + mats <= budget && !(me && std::atoi(me) == 0)) {
+    L.mat_off = uint32_t(L.bytes);
+    L.mats_in_lds = 1;
+    L.bytes += mats;
+  }
+  return L;
 }
 
 // Longest-processing-time-first order of this rank's tiles (zrt.h,
@@ -2022,16 +2145,13 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                                        size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
                                  : c->n_nodes < 65536;
     void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
-    // FAST: at most kStackLdsBytes of LDS stack per block (deep trees keep their
-    // last rows in global memory, rarely touched) so the LDS never caps the
-    // occupancy the registers allow; the other traversals keep it all in LDS
+    // FAST: deep trees keep their last stack rows in global memory (rarely
+    // touched) so the LDS never caps the occupancy the registers allow; the
+    // other traversals keep the whole stack in LDS (zrt::plan_lds)
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    uint32_t lds_rows =
-        mode == 3 ? std::min<uint32_t>(stack_depth, uint32_t(zrt::kStackLdsBytes / (zrt::kBlock * entry)))
-                  : stack_depth;
-    if (mode == 3 && force_rows)
-      lds_rows = std::max<uint32_t>(1, std::min<uint32_t>(lds_rows, uint32_t(std::atoi(force_rows))));
-    const size_t lds = size_t(lds_rows) * zrt::kBlock * entry;
+    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth);
+    const uint32_t lds_rows = lp.stack_rows;
+    const size_t lds = lp.bytes;
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, zrt::kBlock, lds));
     per_cu = std::max(1, std::min(per_cu, 8));
@@ -2047,7 +2167,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint64_t n_partial = uint64_t(my_tiles) * 64u * n_chunks;
     if (c->partial.n < n_partial) c->partial.alloc(n_partial);
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
-    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth) * n_lanes;
+    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_lanes;
     if (att_need * sizeof(float4) > (16ull << 30))
       return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
     if (c->att.n < att_need) c->att.alloc(att_need);
@@ -2098,7 +2218,19 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       a.stack_ovf = c->stack_ovf.p;
     }
     a.n_lanes = uint32_t(n_lanes);
+    a.n_top = c->n_top;
+    a.lds_top_off = lp.top_off;
+    a.lds_att_off = lp.att_off;
+    a.att_lds_rows = lp.att_rows;
+    a.lds_mat_off = lp.mat_off;
+    a.n_mats = c->n_mats;
+    a.mats_in_lds = lp.mats_in_lds;
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
+    if (std::getenv("ZRT_DEBUG_LAUNCH"))
+      std::fprintf(stderr, "zrt launch: mode %d stk16 %d grid %u (%d blocks/CU x %d CUs) lds %zu B "
+                   "(stack rows %u, top nodes %u @%u, att rows %u @%u, mats %u @%u)\n", mode, int(stk16), grid,
+                   per_cu, c->cu_count, lds, lp.stack_rows, c->n_top, lp.top_off, lp.att_rows, lp.att_off,
+                   lp.mats_in_lds ? c->n_mats : 0u, lp.mat_off);
     a.chunk = chunk;
     a.n_chunks = n_chunks;
     a.sync = ZRT_SYNC_SAMPLES;
@@ -2496,11 +2628,8 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
                                        size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
                                  : c->n_nodes < 65536;
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    uint32_t lds_rows =
-        mode == 3 ? std::min<uint32_t>(stack_depth, uint32_t(zrt::kStackLdsBytes / (zrt::kBlock * entry)))
-                  : stack_depth;
-    if (mode == 3 && force_rows)
-      lds_rows = std::max<uint32_t>(1, std::min<uint32_t>(lds_rows, uint32_t(std::atoi(force_rows))));
+    const zrt::LdsPlan lp = zrt::plan_lds(c.get(), mode, stk16, stack_depth, 0);
+    const uint32_t lds_rows = lp.stack_rows;
     const uint32_t grid = (n_rays + zrt::kBlock - 1) / zrt::kBlock;
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
     zrt::DevBuf<float> d_rays, d_t;
@@ -2523,6 +2652,9 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.leaf_of_slot = c->leaf_of_slot.p;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
+    a.n_top = c->n_top;
+    a.lds_top_off = lp.top_off;
+    a.lds_att_off = lp.att_off;
     if (stack_depth > lds_rows) {
       const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
       c->stack_ovf.alloc(ovf_need);
@@ -2538,7 +2670,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     int32_t* sp = d_slot.p;
     uint32_t nn = n_rays;
     void* args[] = {&a, &rp, &nn, &tp, &sp};
-    HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(zrt::kBlock), args, size_t(lds_rows) * zrt::kBlock * entry, c->stream));
+    HIPCHK(hipLaunchKernel(fn, dim3(grid), dim3(zrt::kBlock), args, lp.bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     unsigned long long err = 0;
     HIPCHK(hipMemcpy(&err, c->scratch.p + zrt::kErrorSlot, sizeof(err), hipMemcpyDeviceToHost));
