@@ -202,6 +202,14 @@ typedef struct zrt_stats {
                              (c == k/255, png_image.zig:76-89), else 12 (f32 RGB); 0: no images */
   float schedule_ms;       /* probe + sort before the render launch (included in render_ms) */
   uint64_t order_replays;  /* FAST: rays re-traced the reference's way for an order hazard (diagnostic) */
+  /* REFERENCE traversal + ZRT_FLAG_STATS (diagnostic, DESIGN.md §3 "Exactness"):
+   * over every primitive of every leaf the reference opens, the largest
+   * max(E/t - 1, t/X - 1) of its hit t (t_max = inf) against the leaf box's
+   * loose entry E and exit X - how far rounded hits lie outside their own
+   * box - per primitive kind, and how many hits lie out by more than 2^-14. */
+  float box_excess_max_triangle;
+  float box_excess_max_sphere;
+  uint64_t box_excess_hits;
 } zrt_stats;
 
 /* ---- entry points -------------------------------------------------------- */

@@ -466,3 +466,36 @@ def prim_array(v):
     assert dt.itemsize == C.sizeof(_ffi.Prim)
     buf = (C.c_uint8 * (dt.itemsize * v.n_prims)).from_address(C.addressof(v.prims.contents))
     return np.frombuffer(buf, dtype=dt)
+
+
+def test_trace_order_hazard_band_bit_exact():
+    """rays whose smallest hit is a sphere hit t* lying
+    below its own leaf's loose entry E by a relative (2^-15, 2^-14], with a
+    triangle hit in [t*, E] in an earlier DFS leaf, so the reference rejects the
+    sphere's leaf and returns the triangle (tests/hazard_rays.py).  Every
+    traversal must return the oracle's answer on all of them (and on the 300 000
+    rays around them, half of which show some order effect)."""
+    import hazard_rays as H
+    scene, o, d = H.hazard_scene(1, 300000)
+    c = H.classify(O, scene, o, d)
+    assert c["hazard"].sum() > 200
+    for trav in TRAVERSALS:
+        t, p = z.trace(scene, z.RenderParams(1, 1, 1, 1, traversal=trav), o, d)
+        hz = c["hazard"]
+        assert (p[hz] == c["p_ref"][hz]).all(), f"traversal {trav}: {int((p[hz] != c['p_ref'][hz]).sum())} hazard rays wrong"
+        assert_same_hits(t, p, c["t_ref"], c["p_ref"])
+
+
+def test_reference_box_excess_diagnostic(scenes):
+    """The REFERENCE traversal's STATS flavour measures how far the hits the
+    reference computes lie outside their own leaf's box (zrt_stats.box_excess_*,
+    DESIGN.md §3 "Exactness"): finite, non-negative, identical image."""
+    s = scenes(2)
+    p = z.RenderParams(64, 64, 4, 20, traversal=z.ZRT_TRAVERSAL_REFERENCE)
+    img, _ = z.render(s, s.camera, p)
+    p.flags = z.ZRT_FLAG_STATS
+    img2, st = z.render(s, s.camera, p)
+    assert same_bits(img, img2).all()
+    for k in ("box_excess_max_triangle", "box_excess_max_sphere"):
+        assert np.isfinite(st[k]) and st[k] >= 0.0, (k, st[k])
+    assert st["box_excess_max_triangle"] < 2 ** -12  # the bunny's triangles: far inside FAST's margin

@@ -157,3 +157,19 @@ def test_bvh_hit_reference_test():
     assert 10 < int((p >= 0).sum()) < 1500
     t2, p2 = O.trace(scene, False, rays[:, :3], rays[:, 3:])
     assert (p == p2).all() and ((t == t2) | (np.isinf(t) & np.isinf(t2))).all()
+
+
+def test_hazard_rays_reach_the_band():
+    """tests/hazard_rays.py builds the order hazard round 1's FAST left unguarded:
+    the sphere's rounded hit t* is the smallest hit, its leaf's loose entry E lies
+    in (t* (1 + 2^-15), t* (1 + 2^-14)], and an earlier-DFS triangle hit in
+    [t*, E] makes the reference return the triangle.  Pins that the
+    construction (used by the GPU parity test) produces such rays."""
+    import hazard_rays as H
+    scene, o, d = H.hazard_scene(1, 60000)
+    c = H.classify(O, scene, o, d)
+    assert c["band"].sum() > 200
+    assert c["hazard"].sum() > 40
+    # the reference's answer on a hazard ray is a triangle hit no closer than the sphere's
+    hz = c["hazard"]
+    assert (c["p_ref"][hz] > 0).all()
