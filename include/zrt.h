@@ -166,13 +166,21 @@ typedef struct zrt_params {
  * counts BVH node visits, primitive tests, shaded hits and texel fetches
  * (zrt_stats).  Images are identical; the default flavour counts only the
  * Progress counters (raytrace.zig:20-34). */
-enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u };
+enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u, ZRT_FLAG_SCANLINES = 4u };
 enum { ZRT_DEFAULT_SAMPLE_CHUNK = 32u };
 /* Scheduling (FAST traversal, spp >= 128, unless ZRT_FLAG_NO_SCHEDULE): a probe
  * launch renders 1 sample per pixel of every tile (results discarded) and
  * records each tile's cost; the tiles are radix-sorted by descending cost on
  * the device and the render launch hands out units costliest first, so no long
  * unit starts at the end of the launch.  Images do not depend on it. */
+
+/* ZRT_FLAG_SCANLINES: the launch also counts the recursion-limit hits,
+ * reflections and background hits of every frame row (the deltas that
+ * printProgress prints after each scanline, raytrace.zig:37-50, 184), read
+ * back with zrt_ctx_scanlines / zrt_multi_scanlines / zrt_render_progress.
+ * Images and totals are unchanged; the counts are added per finished work
+ * unit (a few atomics per 8x8 tile x sample chunk), so the flag costs little
+ * but is off in the timed bench. */
 
 /* Progress counters (raytrace.zig:20-34) + timings. */
 typedef struct zrt_stats {
@@ -212,6 +220,20 @@ typedef struct zrt_stats {
   uint64_t box_excess_hits;
 } zrt_stats;
 
+/* One frame row's share of the Progress counters (raytrace.zig:20-34): what
+ * raytrace.zig:184's printProgress(y + 1, ...) reports for scanline y as
+ * deltas (recursion limit, reflections, background hits) and as running sums
+ * (pixels, samples, rays: add rows 0..y).  rays = samples + reflections -
+ * recursion_depth_hits (every rayColor call with depth > 0, raytrace.zig:69). */
+typedef struct zrt_scanline {
+  uint64_t recursion_depth_hits;
+  uint64_t reflections;
+  uint64_t background_hits;
+  uint64_t pixels;
+  uint64_t samples;
+  uint64_t rays;
+} zrt_scanline;
+
 /* ---- entry points -------------------------------------------------------- */
 
 /* Replaces raytrace.render (raytrace.zig:136-203): render the whole frame on
@@ -219,6 +241,12 @@ typedef struct zrt_stats {
  * rng_mode must be ZRT_RNG_COUNTER.  stats may be NULL. */
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera,
                const zrt_params* params, float* out_rgb, zrt_stats* stats);
+
+/* zrt_render that also returns the per-scanline counters of raytrace.zig:184
+ * (scanlines: params->height entries, row 0 = bottom, as the reference's y). */
+int zrt_render_progress(const zrt_scene* scene, const zrt_camera* camera,
+                        const zrt_params* params, float* out_rgb, zrt_stats* stats,
+                        zrt_scanline* scanlines);
 
 /* raytrace.render (raytrace.zig:136-203) over several GPUs of one node, from one
  * host thread: the frame's 8x8 tiles are dealt round-robin
@@ -250,6 +278,9 @@ int zrt_multi_create(const zrt_scene* scene, const zrt_params* params,
 int zrt_multi_render(zrt_multi* multi, const zrt_camera* camera,
                      const zrt_params* params, float* out_rgb, zrt_stats* stats);
 int zrt_multi_destroy(zrt_multi* multi);
+/* Per-scanline counters of the last zrt_multi_render made with
+ * ZRT_FLAG_SCANLINES, summed over the ranks (height = params->height). */
+int zrt_multi_scanlines(zrt_multi* multi, zrt_scanline* out, uint32_t height);
 
 /* The closest-hit query of one rayColor step (raytrace.zig:71-81: the top-level
  * surfaces tested with t_min = 0.001 and a shrinking t_max; under BVH that is
@@ -304,6 +335,11 @@ int zrt_ctx_tile_count(const zrt_ctx* ctx, const zrt_params* params, uint32_t* n
 int zrt_ctx_render_tiles(zrt_ctx* ctx, const zrt_camera* camera,
                          const zrt_params* params, float* dev_tiles,
                          void* hip_stream);
+
+/* This rank's per-scanline counters of the last launch, which must have been
+ * made with ZRT_FLAG_SCANLINES (ZRT_E_INVALID otherwise); out: height entries
+ * (rows of the frame; rows this rank owns no tiles of stay zero). Waits. */
+int zrt_ctx_scanlines(zrt_ctx* ctx, zrt_scanline* out, uint32_t height);
 
 /* Wait for the context's last launch; ZRT_OK, or ZRT_E_UNSUPPORTED when the
  * device reported an error during it (see zrt_ctx_render_tiles). */

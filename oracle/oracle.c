@@ -609,8 +609,8 @@ static uint64_t counter_key(uint64_t pixel, uint32_t sample, uint64_t seed) {
   return ((pixel << 16) | (uint64_t)sample) + seed * 0x9E3779B97F4A7C15ULL;
 }
 
-int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* p,
-                       uint32_t y0, uint32_t y1, float* out, zrt_stats* stats) {
+static int render_rows_impl(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* p,
+                            uint32_t y0, uint32_t y1, float* out, zrt_stats* stats, zrt_scanline* rows) {
   int rc = validate(scene, camera, p);
   if (rc) return rc;
   if (y1 > p->height || y0 > y1) return ZRT_E_INVALID;
@@ -632,6 +632,7 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
   const uint32_t chunk = p->sample_chunk ? p->sample_chunk : ZRT_DEFAULT_SAMPLE_CHUNK;
   for (uint32_t y = y0; y < y1; ++y) {
     const float f_y = (float)y;
+    const Progress prev = c.p;  /* raytrace.zig:185 progress_prev */
     for (uint32_t x = 0; x < p->height; ++x) {  /* raytrace.zig:168 bound */
       const uint64_t offset = (uint64_t)y * p->width + x;
       V3 acc = v3(0.0f, 0.0f, 0.0f);
@@ -667,6 +668,15 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
       out[3 * offset + 1] = px.y;
       out[3 * offset + 2] = px.z;
     }
+    if (rows) {  /* printProgress(y + 1, ...) (raytrace.zig:37-50, 184): this scanline's deltas */
+      zrt_scanline* r = &rows[y];
+      r->recursion_depth_hits = c.p.recursion_depth_hits - prev.recursion_depth_hits;
+      r->reflections = c.p.reflections - prev.reflections;
+      r->background_hits = c.p.background_hits - prev.background_hits;
+      r->pixels = c.p.pixels - prev.pixels;
+      r->samples = c.p.samples - prev.samples;
+      r->rays = c.p.rays - prev.rays;
+    }
   }
   if (stats) {
     memset(stats, 0, sizeof(*stats));
@@ -687,6 +697,20 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const z
   }
   scene_free(&sc);
   return ZRT_OK;
+}
+
+int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* p,
+                       uint32_t y0, uint32_t y1, float* out, zrt_stats* stats) {
+  return render_rows_impl(scene, camera, p, y0, y1, out, stats, NULL);
+}
+
+int oracle_render_scanlines(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* p,
+                            float* out, zrt_stats* stats, zrt_scanline* rows) {
+  if (!p || !rows) return ZRT_E_INVALID;
+  if (out && p->width && p->height)
+    memset(out, 0, sizeof(float) * 3 * (size_t)p->width * p->height);
+  memset(rows, 0, sizeof(zrt_scanline) * p->height);
+  return render_rows_impl(scene, camera, p, 0, p->height, out, stats, rows);
 }
 
 int oracle_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* p,

@@ -47,6 +47,12 @@ int oracle_render_rows(const zrt_scene* scene, const zrt_camera* camera,
                        const zrt_params* params, uint32_t y0, uint32_t y1,
                        float* out_rgb, zrt_stats* stats);
 
+/* The whole frame plus, per scanline y, the Progress deltas printProgress
+ * reports after it (raytrace.zig:37-50, 184-186; rows: height entries). */
+int oracle_render_scanlines(const zrt_scene* scene, const zrt_camera* camera,
+                            const zrt_params* params, float* out_rgb, zrt_stats* stats,
+                            zrt_scanline* rows);
+
 /* BVH built exactly as bvh.zig:62-185, exported in zrt_bvh_node form
  * (pre-order, left first; child < 0 = prim -(c+1)).  Free with oracle_free. */
 int oracle_bvh_build(const zrt_scene* scene, zrt_bvh_node** nodes,

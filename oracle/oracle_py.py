@@ -39,6 +39,8 @@ def load():
                                 C.POINTER(_ffi.Stats)]
     L.oracle_render_rows.argtypes = [S, C.POINTER(_ffi.Camera), C.POINTER(_ffi.Params),
                                      C.c_uint32, C.c_uint32, f3, C.POINTER(_ffi.Stats)]
+    L.oracle_render_scanlines.argtypes = [S, C.POINTER(_ffi.Camera), C.POINTER(_ffi.Params), f3,
+                                          C.POINTER(_ffi.Stats), C.POINTER(_ffi.Scanline)]
     L.oracle_bvh_build.argtypes = [S, C.POINTER(C.POINTER(_ffi.BvhNode)), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]
     L.oracle_camera_init.argtypes = [f3, f3, f3, C.c_float, C.c_float, C.POINTER(_ffi.Camera)]
@@ -94,6 +96,21 @@ def render(scene_view, camera, params, rows=None):
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
     return out, st.as_dict()
+
+
+def render_scanlines(scene_view, camera, params):
+    """oracle_render_scanlines: (image, stats, rows uint64[H, 6]) - the deltas the
+    reference's printProgress reports after each scanline (raytrace.zig:184)."""
+    L = load()
+    p = params.abi() if hasattr(params, "abi") else params
+    out = np.zeros((p.height, p.width, 3), dtype=np.float32)
+    st = _ffi.Stats()
+    rows = (_ffi.Scanline * p.height)()
+    rc = L.oracle_render_scanlines(scene_view, C.byref(camera), C.byref(p),
+                                   out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st), rows)
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_scanlines failed: {rc}")
+    return out, st.as_dict(), np.ctypeslib.as_array(rows).view(np.uint64).reshape(p.height, 6).copy()
 
 
 def bvh_build(scene_view):

@@ -192,3 +192,50 @@ def test_tileframe_ranks_end_to_end(scenes, world):
     assert same_bits(img, ref)
     for k in COUNTERS:
         assert sum(g[2][k] for g in got) == st1[k], k
+
+
+# ---- per-scanline Progress counters (raytrace.zig:37-50, 184; ZRT_FLAG_SCANLINES) ----
+
+@pytest.mark.parametrize("scene_index,dims", [(1, (40, 24, 4, 30)), (2, (48, 40, 8, 20)), (3, (33, 33, 2, 20))],
+                         ids=["list", "bunny", "teapot-ragged"])
+def test_scanlines_match_oracle(scenes, scene_index, dims):
+    """zrt_render_progress: every row's counters equal the deltas the oracle
+    records after each scanline (the reference's printProgress), the image is
+    zrt_render's, and the rows sum to the frame's counters."""
+    s = scenes(scene_index)
+    p = z.RenderParams(*dims)
+    img, st, rows = z.render_progress(s, s.camera, p)
+    plain, st0 = z.render(s, s.camera, p)
+    ref, rst, rrows = O.render_scanlines(s.view, s.camera, p)
+    assert same_bits(img, plain) and same_bits(img, ref)
+    np.testing.assert_array_equal(rows, rrows)
+    tot = rows.sum(axis=0)
+    for i, k in enumerate(("recursion_depth_hits", "reflections", "background_hits", "pixels_processed",
+                           "samples_processed", "rays_processed")):
+        assert tot[i] == st[k] == st0[k] == rst[k], k
+
+
+def test_scanlines_over_ranks(scenes):
+    """Per-rank contexts (tiles round-robin) with ZRT_FLAG_SCANLINES: the ranks'
+    rows sum to the oracle's; a MultiContext sums them itself; a launch without
+    the flag has no rows to read."""
+    s = scenes(2)
+    w, h, spp, depth = 40, 32, 4, 20
+    _, _, rrows = O.render_scanlines(s.view, s.camera, z.RenderParams(w, h, spp, depth))
+    import torch
+    total = np.zeros_like(rrows)
+    for r in range(3):
+        p = z.RenderParams(w, h, spp, depth, rank=r, world_size=3, flags=z.ZRT_FLAG_SCANLINES)
+        ctx = z.RenderContext(s, p)
+        buf = torch.zeros(max(1, ctx.tile_count(p)) * 64 * 3, dtype=torch.float32, device="cuda")
+        ctx.render_tiles(s.camera, p, buf.data_ptr())
+        total += ctx.scanlines(h)
+        ctx.render_tiles(s.camera, z.RenderParams(w, h, spp, depth, rank=r, world_size=3), buf.data_ptr())
+        with pytest.raises(z.ZrtError):
+            ctx.scanlines(h)
+        ctx.close()
+    np.testing.assert_array_equal(total, rrows)
+    m = z.MultiContext(s, z.RenderParams(w, h, spp, depth), [0, 0])
+    m.render(s.camera, z.RenderParams(w, h, spp, depth, flags=z.ZRT_FLAG_SCANLINES))
+    np.testing.assert_array_equal(m.scanlines(h), rrows)
+    m.close()

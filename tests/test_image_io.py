@@ -2,6 +2,7 @@
 command line (main.zig) over the C ABI, and the PNG reader (png_image.zig:19-94).
 CPU-only except the marked test."""
 import os
+import re
 import struct
 import subprocess
 import zlib
@@ -226,3 +227,18 @@ def test_cli_renders_oracle_image(tmp_path, scenes, devices):
                        ("Total background hits", "background_hits"), ("Total pixels", "pixels_processed"),
                        ("Total reflections", "reflections")):
         assert int(summary[label]) == rs[key], label
+    # printProgress after every scanline (raytrace.zig:37-50, 184): the reference's
+    # line format, running pixels / samples / rays, per-row deltas of the rest
+    _, _, rows = O.render_scanlines(s.view, s.camera, z.RenderParams(40, 40, 4, 12))
+    pat = re.compile(r"^Scanline: (\d+)/(\d+) Pixels: (\d+) Samples: (\d+) Rays: (\d+) Recursion limit: (\d+) "
+                     r"Reflections: (\d+) Background hits: (\d+) Pixels/s: \d+\.\d$")
+    lines = [pat.match(line) for line in r.stderr.splitlines() if line.startswith("Scanline:")]
+    assert len(lines) == 40 and all(lines)
+    cum = np.cumsum(rows, axis=0)
+    for y, m in enumerate(lines):
+        v = [int(g) for g in m.groups()]
+        assert v[:2] == [y + 1, 40]
+        assert v[2:5] == [cum[y, 3], cum[y, 4], cum[y, 5]], y  # pixels, samples, rays so far
+        assert v[5:8] == [rows[y, 0], rows[y, 1], rows[y, 2]], y  # this row's limit / reflections / sky
+    order = [line.split(":")[0] for line in r.stderr.splitlines()]
+    assert order.index("Preprocess time") < order.index("Scanline") < order.index("Rendering ready")

@@ -173,3 +173,21 @@ def test_hazard_rays_reach_the_band():
     # the reference's answer on a hazard ray is a triangle hit no closer than the sphere's
     hz = c["hazard"]
     assert (c["p_ref"][hz] > 0).all()
+
+
+def test_oracle_scanlines_are_progress_deltas(scenes):
+    """oracle_render_scanlines: per-row deltas of the Progress counters
+    (raytrace.zig:184-186) that sum to the frame's, with raytrace.zig:168's x bound
+    (height pixels per row) and the same image as oracle_render."""
+    import zraytrace_amd as z
+    s = scenes(1)
+    p = z.RenderParams(24, 16, 4, 30)
+    img, st, rows = O.render_scanlines(s.view, s.camera, p)
+    ref, _ = O.render(s.view, s.camera, p)
+    assert (img.view(np.uint32) == ref.view(np.uint32)).all()
+    assert (rows[:, 3] == 16).all() and (rows[:, 4] == 64).all()
+    assert (rows[:, 5] == rows[:, 4] + rows[:, 1] - rows[:, 0]).all()  # rays = samples + reflections - limit hits
+    tot = rows.sum(axis=0)
+    for i, k in enumerate(("recursion_depth_hits", "reflections", "background_hits", "pixels_processed",
+                           "samples_processed", "rays_processed")):
+        assert tot[i] == st[k], k

@@ -19,7 +19,7 @@ import numpy as np
 from . import _ffi
 from ._ffi import (ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256, ZRT_RNG_COUNTER,  # noqa: F401
                    ZRT_RNG_REFERENCE_STREAM, ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE,
-                   ZRT_TRAVERSAL_BINARY, ZRT_FLAG_STATS, ZRT_FLAG_NO_SCHEDULE,
+                   ZRT_TRAVERSAL_BINARY, ZRT_FLAG_STATS, ZRT_FLAG_NO_SCHEDULE, ZRT_FLAG_SCANLINES,
                    ZrtError, check)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -116,6 +116,25 @@ def render(scene, camera: _ffi.Camera, params: RenderParams):
     return out, st.as_dict()
 
 
+def _scanlines_np(rows) -> np.ndarray:
+    """zrt_scanline[height] -> uint64 array [height, 6] (columns: _ffi.SCANLINE_FIELDS)."""
+    return np.ctypeslib.as_array(rows).view(np.uint64).reshape(len(rows), 6).copy()
+
+
+def render_progress(scene, camera: _ffi.Camera, params: RenderParams):
+    """render() plus the per-scanline Progress counters of raytrace.zig:184
+    (zrt_render_progress): (image, stats, rows uint64[H, 6]: recursion-limit
+    hits, reflections, background hits, pixels, samples, rays of each row)."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+    st = _ffi.Stats()
+    rows = (_ffi.Scanline * params.height)()
+    p = params.abi()
+    check(lib().zrt_render_progress(view, C.byref(camera), C.byref(p),
+                                    out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st), rows))
+    return out, st.as_dict(), _scanlines_np(rows)
+
+
 def render_multi(scene, camera: _ffi.Camera, params: RenderParams, devices):
     """raytrace.render over several GPUs from one process (zrt_render_multi): tiles
     dealt round-robin over `devices`, one RCCL gather to devices[0].  A device
@@ -150,6 +169,12 @@ class MultiContext:
         check(lib().zrt_multi_render(self._h, C.byref(camera), C.byref(p),
                                      out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
         return out, st.as_dict()
+
+    def scanlines(self, height: int) -> np.ndarray:
+        """Per-scanline counters of the last render made with ZRT_FLAG_SCANLINES, summed over ranks."""
+        rows = (_ffi.Scanline * height)()
+        check(lib().zrt_multi_scanlines(self._h, rows, height))
+        return _scanlines_np(rows)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -214,6 +239,12 @@ class RenderContext:
         p = params.abi()
         check(lib().zrt_ctx_assemble_padded(self._h, C.byref(p), C.c_void_p(dev_gathered), stride_tiles,
                                             C.c_void_p(dev_frame), C.c_void_p(stream or None)))
+
+    def scanlines(self, height: int) -> np.ndarray:
+        """This rank's per-scanline counters of the last launch (ZRT_FLAG_SCANLINES)."""
+        rows = (_ffi.Scanline * height)()
+        check(lib().zrt_ctx_scanlines(self._h, rows, height))
+        return _scanlines_np(rows)
 
     def stats(self) -> dict:
         st = _ffi.Stats()

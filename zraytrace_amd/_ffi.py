@@ -31,6 +31,7 @@ ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256 = 0, 1
 ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE, ZRT_TRAVERSAL_BINARY = 0, 1, 2
 ZRT_FLAG_STATS = 1
 ZRT_FLAG_NO_SCHEDULE = 2
+ZRT_FLAG_SCANLINES = 4
 
 
 class Vec3(C.Structure):
@@ -99,6 +100,15 @@ class Stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Scanline(C.Structure):
+    _fields_ = [("recursion_depth_hits", C.c_uint64), ("reflections", C.c_uint64),
+                ("background_hits", C.c_uint64), ("pixels", C.c_uint64), ("samples", C.c_uint64),
+                ("rays", C.c_uint64)]
+
+
+SCANLINE_FIELDS = [name for name, _ in Scanline._fields_]
+
+
 class BvhNode(C.Structure):
     _fields_ = [("min", Vec3), ("left", C.c_int32), ("max", Vec3), ("right", C.c_int32)]
 
@@ -108,6 +118,8 @@ _P = C.c_void_p
 SIGNATURES = [
     ("zrt_render", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                              C.POINTER(C.c_float), C.POINTER(Stats)]),
+    ("zrt_render_progress", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+                                      C.POINTER(C.c_float), C.POINTER(Stats), C.POINTER(Scanline)]),
     ("zrt_render_multi", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
                                    C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_float), C.POINTER(Stats)]),
     ("zrt_multi_create", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_uint32), C.c_uint32,
@@ -115,6 +127,7 @@ SIGNATURES = [
     ("zrt_multi_render", C.c_int, [_P, C.POINTER(Camera), C.POINTER(Params), C.POINTER(C.c_float),
                                    C.POINTER(Stats)]),
     ("zrt_multi_destroy", C.c_int, [_P]),
+    ("zrt_multi_scanlines", C.c_int, [_P, C.POINTER(Scanline), C.c_uint32]),
     ("zrt_trace", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_float), C.c_uint32,
                             C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -130,6 +143,7 @@ SIGNATURES = [
     ("zrt_ctx_assemble", C.c_int, [_P, C.POINTER(Params), _P, _P, _P]),
     ("zrt_ctx_assemble_padded", C.c_int, [_P, C.POINTER(Params), _P, C.c_uint32, _P, _P]),
     ("zrt_ctx_sync", C.c_int, [_P]),
+    ("zrt_ctx_scanlines", C.c_int, [_P, C.POINTER(Scanline), C.c_uint32]),
     ("zrt_ctx_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("zrt_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("zrt_ctx_debug_counters", C.c_int, [_P, C.POINTER(C.c_uint64), C.c_uint32]),

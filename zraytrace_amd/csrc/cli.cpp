@@ -5,10 +5,12 @@
 // A plain client of libzrt.so's C ABI (as a Zig host would be): builds the
 // scene (scenes.zig:267-277 via zrt_scene_load), renders it with zrt_render
 // (raytrace.zig:136-203: BVH on, DefaultPrng seed 42 -> counter RNG), prints
-// the reference's start and summary lines on stderr (raytrace.zig:143-159,
-// 191-201; the per-scanline progress lines of raytrace.zig:37-50 have no
-// counterpart: the frame is one launch) and writes the PNG (main.zig:33,
-// png_image.zig:96-148).  Assets come from $ZRT_ASSETS, else <exe dir>/../assets;
+// the reference's start, per-scanline and summary lines on stderr
+// (raytrace.zig:143-159, 37-50 + 184, 191-201) and writes the PNG (main.zig:33,
+// png_image.zig:96-148).  The scanline lines carry each row's counters as the
+// reference counts them (ZRT_FLAG_SCANLINES, zrt_render_progress); they are
+// printed when the frame is done (it is one launch), and their Pixels/s is the
+// frame's rate, since rows are not rendered one after another.  Assets come from $ZRT_ASSETS, else <exe dir>/../assets;
 // $ZRT_DEVICE picks the GPU, $ZRT_DEVICES="0,1,..." renders over several
 // (zrt_render_multi: tiles round-robin, one RCCL gather).
 #include <unistd.h>
@@ -143,13 +145,23 @@ int main(int argc, char** argv) {
   std::fprintf(stderr, scene->n_prims > 10 ? "Using Bounded Volume Hierarchy\n" : "Using surface list\n");
 
   std::vector<float> image(size_t(width) * height * 3, 0.0f);
+  std::vector<zrt_scanline> rows(height);
   zrt_stats stats;
   const auto t_render = std::chrono::steady_clock::now();
-  rc = devices.empty() ? zrt_render(scene, &camera, &params, image.data(), &stats)
-                       : zrt_render_multi(scene, &camera, &params, devices.data(), uint32_t(devices.size()),
-                                          image.data(), &stats);
+  if (devices.empty()) {
+    rc = zrt_render_progress(scene, &camera, &params, image.data(), &stats, rows.data());
+  } else {
+    params.flags |= ZRT_FLAG_SCANLINES;
+    zrt_multi* multi = nullptr;
+    rc = zrt_multi_create(scene, &params, devices.data(), uint32_t(devices.size()), &multi);
+    if (rc == ZRT_OK) rc = zrt_multi_render(multi, &camera, &params, image.data(), &stats);
+    if (rc == ZRT_OK) rc = zrt_multi_scanlines(multi, rows.data(), height);
+    const std::string msg = zrt_last_error();
+    zrt_multi_destroy(multi);
+    if (rc != ZRT_OK) std::fprintf(stderr, "error: %s\n", msg.c_str());
+  }
   if (rc != ZRT_OK) {
-    std::fprintf(stderr, "error: %s\n", zrt_last_error());
+    if (devices.empty()) std::fprintf(stderr, "error: %s\n", zrt_last_error());
     zrt_scene_free(data);
     return 1;
   }
@@ -157,6 +169,20 @@ int main(int argc, char** argv) {
   const double call = seconds_since(t_render);
   const double render_runtime = stats.render_ms / 1000.0;  // the sampling loop itself
   std::fprintf(stderr, "Preprocess time: %.2f seconds\n", runtime - render_runtime);
+  // printProgress after every scanline (raytrace.zig:37-50, 184)
+  const double pixels_per_second = double(stats.pixels_processed) / render_runtime;
+  unsigned long long pixels = 0, samples_sum = 0, rays = 0;
+  for (uint32_t y = 0; y < height; ++y) {
+    pixels += rows[y].pixels;
+    samples_sum += rows[y].samples;
+    rays += rows[y].rays;
+    std::fprintf(stderr,
+                 "Scanline: %u/%u Pixels: %llu Samples: %llu Rays: %llu Recursion limit: %llu Reflections: %llu "
+                 "Background hits: %llu Pixels/s: %.1f\n",
+                 y + 1, unsigned(height), pixels, samples_sum, rays,
+                 (unsigned long long)rows[y].recursion_depth_hits, (unsigned long long)rows[y].reflections,
+                 (unsigned long long)rows[y].background_hits, pixels_per_second);
+  }
   std::fprintf(stderr, "Rendering ready\n");
   std::fprintf(stderr, "  Total reflections:     %llu\n", (unsigned long long)stats.reflections);
   std::fprintf(stderr, "  Total background hits: %llu\n", (unsigned long long)stats.background_hits);

@@ -78,6 +78,9 @@ struct KArgs {
   const uint32_t* __restrict__ tile_order;  // local tiles in the order units are handed out, or null
   unsigned long long* __restrict__ wave_times;  // ZRT_PROFILE builds: {start, end} realtime per wave
   unsigned long long* __restrict__ counters;  // kNumCounters x u64
+  // ZRT_FLAG_SCANLINES: [row][3] recursion-limit hits, reflections, background
+  // hits per frame row (raytrace.zig:184's printProgress deltas), else null
+  unsigned long long* __restrict__ scanlines;
   uint32_t* __restrict__ error_flag;
   float org[3], llc[3], hor[3], ver[3];
   float f_width, f_height, color_scale, pad0;
@@ -745,8 +748,8 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
 #define ZRT_LOAD_NODE(Q)                                                       \
   nx = Q[0]; ny = Q[1]; nz = Q[2]; fx = Q[3]; fy = Q[4]; fz = Q[5]; ra = Q[6];
 #else
-  const uint32_t base = 0;
-#define ZRT_LOAD_NODE(Q)                                                       \
+  const uint32_t oct = 0, base = 0;
+#define ZRT_LOAD_NODE(Q)                                                      \
   {                                                                            \
     const float4 m0 = Q[0], m1 = Q[1], m2 = Q[2], m3 = Q[3], m4 = Q[4], m5 = Q[5]; \
     nx = sx ? m3 : m0; fx = sx ? m0 : m3;                                      \
@@ -975,6 +978,24 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
   if (__lane_id() == 0 && (lo | hi)) atomicAdd(dst, ((unsigned long long)hi << 32) | lo);
 }
 
+// ZRT_FLAG_SCANLINES: a finished unit's counters added to its frame rows.  The
+// 8 lanes of a tile row (lanes 8k .. 8k+7) are summed with shuffles, then one
+// lane per row adds them.  Called with the whole wave converged.
+__device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ rows, uint32_t py, uint32_t height,
+                                               int lane, uint32_t d, uint32_t r, uint32_t b) {
+#pragma unroll
+  for (int off = 1; off <= 4; off <<= 1) {
+    d += __shfl_xor(d, off);
+    r += __shfl_xor(r, off);
+    b += __shfl_xor(b, off);
+  }
+  if ((lane & 7) == 0 && py < height) {
+    if (d) atomicAdd(&rows[3 * py + 0], (unsigned long long)d);
+    if (r) atomicAdd(&rows[3 * py + 1], (unsigned long long)r);
+    if (b) atomicAdd(&rows[3 * py + 2], (unsigned long long)b);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // the sampling loop
 // ---------------------------------------------------------------------------
@@ -1041,6 +1062,10 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         gate = min(gate + a.sync, unit_end);
       } else {
         if (a.unit_cost && cur_lt != 0xffffffffu && lane == 0) a.unit_cost[cur_lt] = iters;
+        if (a.scanlines && cur_lt != 0xffffffffu) {  // the finished unit's counters, per frame row
+          flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
+          c_depth = c_refl = c_bg = 0;  // (so the launch totals are the rows' sums)
+        }
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.work_counter, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
@@ -1590,6 +1615,8 @@ struct zrt_ctx {
   uint32_t tile_ids_n = 0;
   zrt::DevBuf<unsigned long long> wave_times;  // ZRT_PROFILE builds
   uint32_t n_waves = 0;
+  zrt::DevBuf<unsigned long long> scanlines;  // ZRT_FLAG_SCANLINES: [row][3] of the last launch
+  uint32_t scanline_rows = 0;                 // rows counted by the last launch (0: not flagged)
   bool scheduled = false;
   hipEvent_t ev_pre = nullptr, ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
   double preprocess_ms = 0, upload_ms = 0;
@@ -1598,6 +1625,7 @@ struct zrt_ctx {
   unsigned long long* err_host = nullptr;
   bool err_reported = false;  // the last launch's device error was returned to the caller
   uint32_t last_pixels = 0, last_spp = 0, launched = 0;
+  uint32_t last_tiles = 0, last_rank = 0, last_world = 1, last_tiles_x = 0, last_xbound = 0;
   bool last_stats = false;
   int last_mode = 0;
   int cu_count = 0;
@@ -2304,6 +2332,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.chunk = chunk;
     a.n_chunks = n_chunks;
     a.sync = ZRT_SYNC_SAMPLES;
+    if (const char* e = std::getenv("ZRT_SYNC"))  // A/B: lockstep interval in samples (identical images)
+      a.sync = std::max(1u, uint32_t(std::atoi(e)));
     a.n_slots = my_tiles * 64u;
 
     HIPCHK(hipEventRecord(c->ev_pre, st));
@@ -2311,6 +2341,13 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
         mode == 3 && !(p->flags & ZRT_FLAG_NO_SCHEDULE) && p->samples_per_pixel >= 128 && my_tiles >= 2;
     c->scheduled = schedule;
     if (schedule) zrt::schedule_tiles(c, a, p->prng, stk16, my_tiles, grid, lds, st);
+    c->scanline_rows = 0;
+    if (p->flags & ZRT_FLAG_SCANLINES) {  // (not the probe's: set after it)
+      if (c->scanlines.n < size_t(p->height) * 3) c->scanlines.alloc(size_t(p->height) * 3);
+      HIPCHK(hipMemsetAsync(c->scanlines.p, 0, size_t(p->height) * 3 * sizeof(unsigned long long), st));
+      a.scanlines = c->scanlines.p;
+      c->scanline_rows = p->height;
+    }
     if (ZRT_PROFILE) {
       c->n_waves = grid * (zrt::kBlock / 64);
       if (c->wave_times.n < 2ull * c->n_waves) c->wave_times.alloc(2ull * c->n_waves);
@@ -2343,6 +2380,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     }
     c->last_pixels = uint32_t(pixels);
     c->last_spp = p->samples_per_pixel;
+    c->last_tiles = my_tiles;
+    c->last_rank = p->rank;
+    c->last_world = p->world_size;
+    c->last_tiles_x = g.tiles_x;
+    c->last_xbound = g.xbound;
     c->last_stats = diag;
     c->last_mode = mode;
     c->launched = 1;
@@ -2359,6 +2401,15 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     HIPCHK(hipEventSynchronize(c->ev_done));
     unsigned long long h[zrt::kScratchSlots] = {0};
     HIPCHK(hipMemcpy(h, c->scratch.p, sizeof(h), hipMemcpyDeviceToHost));
+    if (c->scanline_rows) {  // ZRT_FLAG_SCANLINES: the launch counted these three per row only
+      std::vector<unsigned long long> rows(size_t(c->scanline_rows) * 3);
+      HIPCHK(hipMemcpy(rows.data(), c->scanlines.p, rows.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      for (size_t y = 0; y < c->scanline_rows; ++y) {
+        h[zrt::kDepthHits] += rows[3 * y];
+        h[zrt::kReflections] += rows[3 * y + 1];
+        h[zrt::kBackground] += rows[3 * y + 2];
+      }
+    }
     std::memset(out, 0, sizeof(*out));
     out->recursion_depth_hits = h[zrt::kDepthHits];
     out->reflections = h[zrt::kReflections];
@@ -2403,6 +2454,51 @@ int zrt_ctx_sync(zrt_ctx* c) {
   if (!c) return fail(ZRT_E_INVALID, "null argument");
   try {
     HIPCHK(hipSetDevice(c->device));
+    return zrt::launch_status(c, true);
+  }
+  ZRT_CATCH_ALL
+}
+
+namespace zrt {
+namespace {
+// The per-row Progress counters of c's last launch (ZRT_FLAG_SCANLINES) added
+// into out[0 .. height): this rank's pixels, samples and rays of each row and
+// the three counters the kernel counted per row.
+int add_scanlines(zrt_ctx* c, zrt_scanline* out, uint32_t height) {
+  if (!c->launched || c->scanline_rows == 0)
+    return fail(ZRT_E_INVALID, "the last launch did not count scanlines (ZRT_FLAG_SCANLINES)");
+  if (height != c->scanline_rows) return fail(ZRT_E_INVALID, "height differs from the last launch's");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->ev_done));
+  std::vector<unsigned long long> rows(size_t(height) * 3);
+  HIPCHK(hipMemcpy(rows.data(), c->scanlines.p, rows.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (uint32_t lt = 0; lt < c->last_tiles; ++lt) {  // pixels of this rank's tiles, per row
+    const uint32_t t = lt * c->last_world + c->last_rank;
+    const uint32_t tx = t % c->last_tiles_x, ty = t / c->last_tiles_x;
+    const uint32_t w = std::min(8u, c->last_xbound - tx * 8u);
+    for (uint32_t y = ty * 8u; y < std::min(height, ty * 8u + 8u); ++y) out[y].pixels += w;
+  }
+  for (uint32_t y = 0; y < height; ++y) {
+    out[y].recursion_depth_hits += rows[3 * y];
+    out[y].reflections += rows[3 * y + 1];
+    out[y].background_hits += rows[3 * y + 2];
+  }
+  // samples and rays from the pixels (rays = rayColor calls - depth-limit hits)
+  for (uint32_t y = 0; y < height; ++y) {
+    out[y].samples = out[y].pixels * uint64_t(c->last_spp);
+    out[y].rays = out[y].samples + out[y].reflections - out[y].recursion_depth_hits;
+  }
+  return ZRT_OK;
+}
+}  // namespace
+}  // namespace zrt
+
+int zrt_ctx_scanlines(zrt_ctx* c, zrt_scanline* out, uint32_t height) {
+  if (!c || !out) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    std::memset(out, 0, sizeof(zrt_scanline) * height);
+    int rc = zrt::add_scanlines(c, out, height);
+    if (rc) return rc;
     return zrt::launch_status(c, true);
   }
   ZRT_CATCH_ALL
@@ -2475,14 +2571,17 @@ int zrt_ctx_assemble_padded(zrt_ctx* c, const zrt_params* p, const float* dev_ga
   return zrt::assemble(c, p, dev_gathered, stride_tiles, dev_frame, hip_stream);
 }
 
-int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
-               float* out_rgb, zrt_stats* stats) {
+namespace zrt {
+namespace {
+int render_one(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params, float* out_rgb,
+               zrt_stats* stats, zrt_scanline* rows) {
   if (!camera || !out_rgb) return fail(ZRT_E_INVALID, "null argument");
   int rc = zrt::validate_params(params);
   if (rc) return rc;
   zrt_params p = *params;
   p.rank = 0;
   p.world_size = 1;
+  if (rows) p.flags |= ZRT_FLAG_SCANLINES;
   zrt_ctx* c = nullptr;
   rc = zrt_ctx_create(scene, &p, &c);
   if (rc) return rc;
@@ -2503,10 +2602,28 @@ int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_param
     zrt_stats s;
     rc = zrt_ctx_stats(c, &s);
     if (rc) return rc;
+    if (rows) {
+      std::memset(rows, 0, sizeof(zrt_scanline) * p.height);
+      rc = add_scanlines(c, rows, p.height);
+      if (rc) return rc;
+    }
     if (stats) *stats = s;
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
+}
+}  // namespace
+}  // namespace zrt
+
+int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
+               float* out_rgb, zrt_stats* stats) {
+  return zrt::render_one(scene, camera, params, out_rgb, stats, nullptr);
+}
+
+int zrt_render_progress(const zrt_scene* scene, const zrt_camera* camera, const zrt_params* params,
+                        float* out_rgb, zrt_stats* stats, zrt_scanline* scanlines) {
+  if (!scanlines) return fail(ZRT_E_INVALID, "null argument");
+  return zrt::render_one(scene, camera, params, out_rgb, stats, scanlines);
 }
 
 // ---- several GPUs from one host thread (zrt_multi_*, zrt_render_multi) -------
@@ -2659,6 +2776,19 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
     sum.n_gpus = m->n_distinct;
     if (stats) *stats = sum;
     if (device_rc) return fail(device_rc, zrt::kOverflowMsg);
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_multi_scanlines(zrt_multi* m, zrt_scanline* out, uint32_t height) {
+  if (!m || !out) return fail(ZRT_E_INVALID, "null argument");
+  try {
+    std::memset(out, 0, sizeof(zrt_scanline) * height);
+    for (auto& c : m->ctx) {
+      const int rc = zrt::add_scanlines(c.get(), out, height);
+      if (rc) return rc;
+    }
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
