@@ -102,12 +102,18 @@ struct KArgs {
   uint32_t att_lds_rows;  //   (rows att_lds_rows.. in `att`, [row - att_lds_rows][lane])
   uint32_t lds_mat_off;   // the material table (n_mats DevMaterial), when mats_in_lds
   uint32_t n_mats, mats_in_lds;
+  uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
        kLeaves, kReplays, kExcessTri, kExcessSph, kExcessHits, kNumCounters };
 constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 24;
+// STATS flavour, SIMD efficiency (zrt_ctx_debug_counters): traversal loop trips
+// of the waves (per traced step, the most node visits of any lane: kNodes /
+// (64 kTravTrips) is the lane efficiency of traversal), loop iterations in which
+// some lane ran a rayColor step, and the lane-steps run in them
+constexpr int kTravTrips = 21, kLoopTrips = 22, kLaneSteps = 23;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
 // cycle sums per loop section into counters[kProfSlot + section].
@@ -728,11 +734,79 @@ __device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict
 // test still uses the current best with lower-slot tie-breaking); leaf slots
 // are intersected in place, inner slots are sorted by entry distance and the
 // farther ones pushed, branch-free.
+// One wide node's record in registers: the four slots' near planes, far planes
+// (per axis, pre-swapped in the ray's octant copy) and primitive/child refs.
+struct WideNode {
+  float4 nx, ny, nz, fx, fy, fz, ra;
+};
+
+__device__ __forceinline__ void wide_load(const float4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
+#if ZRT_OCT_COPIES
+  (void)sx; (void)sy; (void)sz;
+  w.nx = q[0]; w.ny = q[1]; w.nz = q[2]; w.fx = q[3]; w.fy = q[4]; w.fz = q[5]; w.ra = q[6];
+#else
+  const float4 m0 = q[0], m1 = q[1], m2 = q[2], m3 = q[3], m4 = q[4], m5 = q[5];
+  w.nx = sx ? m3 : m0; w.fx = sx ? m0 : m3;
+  w.ny = sy ? m4 : m1; w.fy = sy ? m1 : m4;
+  w.nz = sz ? m5 : m2; w.fz = sz ? m2 : m5;
+  w.ra = q[6];
+#endif
+}
+
+// Where a ray reads the wide tree: its octant's copy (global memory) and that
+// copy's top levels in LDS.
+struct WideView {
+  const float4* __restrict__ top;  // this octant's copy of the top nodes in LDS
+  uint32_t base;                   // float4 offset of this octant's copy (< 2^32)
+  uint32_t n_top;
+  bool sx, sy, sz;
+};
+
+__device__ __forceinline__ WideView wide_view(const KArgs& a, const RayT& r, const float4* __restrict__ lds_top) {
+  WideView v;
+  v.sx = r.ix < 0.0f;
+  v.sy = r.iy < 0.0f;
+  v.sz = r.iz < 0.0f;
+#if ZRT_OCT_COPIES
+  const uint32_t oct = (v.sx ? 1u : 0u) | (v.sy ? 2u : 0u) | (v.sz ? 4u : 0u);
+  v.base = oct * a.wide_stride;
+#else
+  const uint32_t oct = 0;
+  v.base = 0;
+#endif
+  v.top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
+  v.n_top = ZRT_LDS_TOP ? a.n_top : 0u;
+  return v;
+}
+
+// The address of wide node `i` for this ray: LDS for a top-level node, else
+// its octant copy in global memory.
+__device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const WideView& v, uint32_t i) {
+  return i < v.n_top ? v.top + 8u * i : a.wnodes + (v.base + 8u * i);
+}
+
+// FAST: near-first over the 4-wide tree (accel_build.cpp), stored once per
+// ray octant with each axis' min / max planes swapped where the octant's
+// direction is negative, so a node's first three float4 are the four slots'
+// near planes and the next three their far planes: the reference's swap
+// (aabb.zig:116-118) is done by the layout, not per slot.  All four slots are
+// tested against the t_max at node entry (a leaf passing with a t_max >= the
+// current one is a superset of what the reference opens, and every primitive
+// test still uses the current best with lower-slot tie-breaking); leaf slots
+// are intersected in place, inner slots are sorted by entry distance and the
+// farther ones pushed, branch-free.
+//
+// wide_iter processes the node in `w` (read from q), picks the next node
+// (pushing the farther inner children), intersects the opened leaves and loads
+// the next node into `w` / q.  Returns false when the traversal is over (then
+// the order-hazard test of wide_finish follows).  Its state between calls is
+// (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
+// suspended between nodes (the wavefront loop, render_loop_wf).
 template <bool STATS, class StackT>
-__device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
-                                              const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
-                                              int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
-                                              uint32_t& c_sph, uint32_t& c_replays) {
+__device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
+                                          StackT* __restrict__ stk, uint32_t gl, WideNode& w,
+                                          const float4*& q, uint32_t& sp, float& best_t, int& best,
+                                          uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
   // the first rows in LDS, the rest in global memory (32-bit stacks only: the
@@ -741,114 +815,90 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const uint32_t rows = kOvf ? a.lds_rows : cap;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float inf = __builtin_inff();
-  const bool sx = r.ix < 0.0f, sy = r.iy < 0.0f, sz = r.iz < 0.0f;
-#if ZRT_OCT_COPIES
-  const uint32_t oct = (sx ? 1u : 0u) | (sy ? 2u : 0u) | (sz ? 4u : 0u);
-  const uint32_t base = oct * a.wide_stride;  // float4 offset of this octant's copy (< 2^32)
-#define ZRT_LOAD_NODE(Q)                                                       \
-  nx = Q[0]; ny = Q[1]; nz = Q[2]; fx = Q[3]; fy = Q[4]; fz = Q[5]; ra = Q[6];
-#else
-  const uint32_t oct = 0, base = 0;
-#define ZRT_LOAD_NODE(Q)                                                      \
-  {                                                                            \
-    const float4 m0 = Q[0], m1 = Q[1], m2 = Q[2], m3 = Q[3], m4 = Q[4], m5 = Q[5]; \
-    nx = sx ? m3 : m0; fx = sx ? m0 : m3;                                      \
-    ny = sy ? m4 : m1; fy = sy ? m1 : m4;                                      \
-    nz = sz ? m5 : m2; fz = sz ? m2 : m5;                                      \
-    ra = Q[6];                                                                 \
-  }
-#endif
-  uint32_t sp = 0;
-  // this octant's copy of the top nodes in LDS; the root is its node 0
-  const float4* __restrict__ top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
-  const uint32_t n_top = ZRT_LDS_TOP ? a.n_top : 0u;
-  const float4* q = ZRT_LDS_TOP ? top : a.wnodes + base;
-  float4 nx, ny, nz, fx, fy, fz, ra;
-  ZRT_LOAD_NODE(q)
-  for (;;) {
-    int r0 = as_int(ra.x), r1 = as_int(ra.y), r2 = as_int(ra.z), r3 = as_int(ra.w);
-    const float tb = __builtin_fabsf(best_t) * kOpen;
+  const bool sx = v.sx, sy = v.sy, sz = v.sz;
+  int r0 = as_int(w.ra.x), r1 = as_int(w.ra.y), r2 = as_int(w.ra.z), r3 = as_int(w.ra.w);
+  const float tb = __builtin_fabsf(best_t) * kOpen;
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
-    const f2 nx01 = ZRT_SLAB_X(nx, x, y), nx23 = ZRT_SLAB_X(nx, z, w);
-    const f2 ny01 = ZRT_SLAB_Y(ny, x, y), ny23 = ZRT_SLAB_Y(ny, z, w);
-    const f2 nz01 = ZRT_SLAB_Z(nz, x, y), nz23 = ZRT_SLAB_Z(nz, z, w);
-    const f2 fx01 = ZRT_SLAB_X(fx, x, y), fx23 = ZRT_SLAB_X(fx, z, w);
-    const f2 fy01 = ZRT_SLAB_Y(fy, x, y), fy23 = ZRT_SLAB_Y(fy, z, w);
-    const f2 fz01 = ZRT_SLAB_Z(fz, x, y), fz23 = ZRT_SLAB_Z(fz, z, w);
+  const f2 nx01 = ZRT_SLAB_X(w.nx, x, y), nx23 = ZRT_SLAB_X(w.nx, z, w);
+  const f2 ny01 = ZRT_SLAB_Y(w.ny, x, y), ny23 = ZRT_SLAB_Y(w.ny, z, w);
+  const f2 nz01 = ZRT_SLAB_Z(w.nz, x, y), nz23 = ZRT_SLAB_Z(w.nz, z, w);
+  const f2 fx01 = ZRT_SLAB_X(w.fx, x, y), fx23 = ZRT_SLAB_X(w.fx, z, w);
+  const f2 fy01 = ZRT_SLAB_Y(w.fy, x, y), fy23 = ZRT_SLAB_Y(w.fy, z, w);
+  const f2 fz01 = ZRT_SLAB_Z(w.fz, x, y), fz23 = ZRT_SLAB_Z(w.fz, z, w);
 #undef ZRT_SLAB_X
 #undef ZRT_SLAB_Y
 #undef ZRT_SLAB_Z
-    const SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
-    const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
-    const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
-    const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
-    // narrowed test: entry > exit * (1 + 2^-16) culls
-    const bool h0 = !(s0.en > s0.ex * 1.0000153f), h1 = !(s1.en > s1.ex * 1.0000153f);
-    const bool h2 = !(s2.en > s2.ex * 1.0000153f), h3 = !(s3.en > s3.ex * 1.0000153f);
-    if (STATS) {
-      ++c_nodes;
-      c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
-    }
-    // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
-    bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
-    const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
-    const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
-    if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-      if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
-      if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
-      if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
-      if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
-    }
-    const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
-    const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
-    int32_t next = -1;
-    // inner slots that pass, keyed by entry distance
-    float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
-    float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
-    const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
-    // sort (entry, ref) ascending: 5 compare-exchanges
-    cswap(k0, r0, k1, r1);
-    cswap(k2, r2, k3, r3);
-    cswap(k0, r0, k2, r2);
-    cswap(k1, r1, k3, r3);
-    cswap(k1, r1, k2, r2);
-    if (n != 0) {
-      // push r_{n-1} .. r_1 (farthest first) and continue with the nearest; the
-      // three stores are unconditional (entries above the new top are dead)
-      const StackT e0 = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1), e1 = (StackT)(n == 4 ? r2 : r1);
-      const StackT e2 = (StackT)r1;
-      // sp <= cap - 3 always holds (the clamp below), so the three stores stay in the rows
-      if (sp + 3 <= rows) {
-        stk[sp * stride] = e0;
-        stk[(sp + 1) * stride] = e1;
-        stk[(sp + 2) * stride] = e2;
-      } else if (kOvf) {  // deep trees: rows past the LDS part live in global memory
-        const StackT e[3] = {e0, e1, e2};
+  const SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
+  const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
+  const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
+  const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
+  // narrowed test: entry > exit * (1 + 2^-16) culls
+  const bool h0 = !(s0.en > s0.ex * 1.0000153f), h1 = !(s1.en > s1.ex * 1.0000153f);
+  const bool h2 = !(s2.en > s2.ex * 1.0000153f), h3 = !(s3.en > s3.ex * 1.0000153f);
+  if (STATS) {
+    ++c_nodes;
+    c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
+  }
+  // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
+  bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
+  const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
+  const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
+  if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
+    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
+    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
+    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
+    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
+  }
+  const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
+  const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
+  int32_t next = -1;
+  // inner slots that pass, keyed by entry distance
+  float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
+  float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
+  const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
+  // sort (entry, ref) ascending: 5 compare-exchanges
+  cswap(k0, r0, k1, r1);
+  cswap(k2, r2, k3, r3);
+  cswap(k0, r0, k2, r2);
+  cswap(k1, r1, k3, r3);
+  cswap(k1, r1, k2, r2);
+  if (n != 0) {
+    // push r_{n-1} .. r_1 (farthest first) and continue with the nearest; the
+    // three stores are unconditional (entries above the new top are dead)
+    const StackT e0 = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1), e1 = (StackT)(n == 4 ? r2 : r1);
+    const StackT e2 = (StackT)r1;
+    // sp <= cap - 3 always holds (the clamp below), so the three stores stay in the rows
+    if (sp + 3 <= rows) {
+      stk[sp * stride] = e0;
+      stk[(sp + 1) * stride] = e1;
+      stk[(sp + 2) * stride] = e2;
+    } else if (kOvf) {  // deep trees: rows past the LDS part live in global memory
+      const StackT e[3] = {e0, e1, e2};
 #pragma unroll
-        for (uint32_t j = 0; j < 3; ++j) {
-          if (sp + j < rows) stk[(sp + j) * stride] = e[j];
-          else ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
-        }
+      for (uint32_t j = 0; j < 3; ++j) {
+        if (sp + j < rows) stk[(sp + j) * stride] = e[j];
+        else ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
       }
-      const uint32_t nsp = sp + n - 1;
-      // the host sizes cap = the tree's deepest stack + 3, so this never fires
-      // unless the stack was sized too small: then entries would be lost
-      if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, 1u);
-      sp = min(nsp, cap - 3);
-      next = r0;
-    } else if (sp != 0) {
-      --sp;
-      next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
     }
-    // each lane walks ITS opened leaves in slot order, so lanes that opened
-    // different slots share loop trips (the result is the closest t, ties to
-    // the lower slot, order hazards flagged).  A/B against four unrolled slot
-    // blocks: C5 +2.9 %, C3 +3.2 %, C4 -0.2 % (and one copy of the tests).
-    if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
-      uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
-      if (open != 0) {
+    const uint32_t nsp = sp + n - 1;
+    // the host sizes cap = the tree's deepest stack + 3, so this never fires
+    // unless the stack was sized too small: then entries would be lost
+    if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, 1u);
+    sp = min(nsp, cap - 3);
+    next = r0;
+  } else if (sp != 0) {
+    --sp;
+    next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+  }
+  // each lane walks ITS opened leaves in slot order, so lanes that opened
+  // different slots share loop trips (the result is the closest t, ties to
+  // the lower slot, order hazards flagged).  A/B against four unrolled slot
+  // blocks: C5 +2.9 %, C3 +3.2 %, C4 -0.2 % (and one copy of the tests).
+  if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
+    uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
+    if (open != 0) {
       const float4 rb = leaf_q[7];
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(open);
@@ -859,9 +909,9 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
         prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);
         if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
       } while (open != 0);
-      }
-    } else if ((l0 | l1 | l2 | l3) != 0) {
-      const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
+    }
+  } else if ((l0 | l1 | l2 | l3) != 0) {
+    const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
 #define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
   if (L != 0) {                                                                                     \
     const int pb = as_int(RB);                                                                      \
@@ -869,25 +919,31 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);              \
     if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp); \
   }
-      ZRT_WIDE_LEAF(l0, rb.x, 0)
-      ZRT_WIDE_LEAF(l1, rb.y, 1)
-      ZRT_WIDE_LEAF(l2, rb.z, 2)
-      ZRT_WIDE_LEAF(l3, rb.w, 3)
+    ZRT_WIDE_LEAF(l0, rb.x, 0)
+    ZRT_WIDE_LEAF(l1, rb.y, 1)
+    ZRT_WIDE_LEAF(l2, rb.z, 2)
+    ZRT_WIDE_LEAF(l3, rb.w, 3)
 #undef ZRT_WIDE_LEAF
-    }
-    if (next < 0) break;
-    if ((uint32_t)next < n_top) {  // a top-level node: from LDS (ds_read)
-      const float4* __restrict__ t = top + 8u * (uint32_t)next;
-      q = t;
-      ZRT_LOAD_NODE(t)
-    } else {
-      const float4* __restrict__ g = a.wnodes + (base + 8u * (uint32_t)next);
-      q = g;
-      ZRT_LOAD_NODE(g)
-    }
   }
-#undef ZRT_LOAD_NODE
-  if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best), 0)) {  // 1e-8..1e-5 of rays
+  if (next < 0) return false;
+  if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS (ds_read)
+    const float4* __restrict__ t = v.top + 8u * (uint32_t)next;
+    q = t;
+    wide_load(t, sx, sy, sz, w);
+  } else {
+    const float4* __restrict__ g = a.wnodes + (v.base + 8u * (uint32_t)next);
+    q = g;
+    wide_load(g, sx, sy, sz, w);
+  }
+  return true;
+}
+
+// The end of a FAST traversal: the order hazard of DESIGN.md §3 (1e-8..1e-5
+// of rays) re-traced the reference's way.
+template <bool STATS, class StackT>
+__device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, StackT* __restrict__ stk, uint32_t gl,
+                                            float& best_t, int& best, uint32_t& c_replays) {
+  if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best), 0)) {
     if (STATS) ++c_replays;
 #if ZRT_REPLAY_OFF
     best_t = -best_t;  // A/B only: the replay's cost without its code (results not exact)
@@ -895,6 +951,22 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
     reference_replay<StackT>(a, r, stk, gl, best_t, best);
 #endif
   }
+}
+
+template <bool STATS, class StackT>
+__device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
+                                              const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
+                                              int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
+                                              uint32_t& c_sph, uint32_t& c_replays) {
+  const WideView v = wide_view(a, r, lds_top);
+  uint32_t sp = 0;
+  // the root is node 0 of this octant's copy (in LDS when the top levels are)
+  const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+  WideNode w;
+  wide_load(q, v.sx, v.sy, v.sz, w);
+  while (wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph)) {
+  }
+  wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
 
 // ---------------------------------------------------------------------------
@@ -1012,6 +1084,118 @@ constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 #define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B (octant traversal, 96 VGPRs): w4 46.0, w5 50.6, w6 48.2 (spills) Gray/s
 #endif
 
+// The rest of one rayColor step after its closest-hit query (raytrace.zig:
+// 71-100): a miss is the sky (backgroundColor); a hit is HitRecord.init
+// (hit_record.zig:28-41) + Material.scatter (material.zig:43-129): absorbed
+// ends the path black, a scatter pushes its attenuation (the product is taken
+// in the recursion's order when the path ends) and moves the ray on.
+template <bool STATS, class R>
+__device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __restrict__ mats,
+                                           float* __restrict__ att_l, uint32_t gl, R& rng, int best, float best_t,
+                                           V3& o, V3& d, uint32_t& depth_left, bool& path_end, bool& sky, V3& L,
+                                           uint32_t& c_bg, uint32_t& c_refl, uint32_t& c_shade, uint32_t& c_tex) {
+  if (best < 0) {
+    ++c_bg;
+    L = background(d);
+    path_end = true;
+    sky = true;
+  } else {
+    // ---- HitRecord.init (hit_record.zig:28-41)
+    const float4 sh = a.shade[best];
+    const uint32_t tag = __float_as_uint(sh.w);
+    const MatReg mat = load_material(mats, tag & 0x7fffffffu);
+    const uint32_t mkind = mat.kind();
+    const bool need_uv = mkind != ZRT_MAT_DIELECTRIC && mat.tex_kind() == ZRT_TEX_IMAGE;
+    if (STATS) {
+      ++c_shade;
+      c_tex += need_uv ? 1u : 0u;
+    }
+    const V3 loc = add(o, scale(d, best_t));
+    V3 outward;
+    float tu = 0.0f, tv = 0.0f;
+    if (tag >> 31) {
+      outward = mk(sh.x, sh.y, sh.z);  // face_unit_normal
+      if (need_uv) {  // barycentric (u, v), same arithmetic as the hit test
+        const float4 p0 = a.prims[3 * best + 0];
+        const float4 p1 = a.prims[3 * best + 1];
+        const float4 p2 = a.prims[3 * best + 2];
+        const V3 n = mk(p2.y, p2.z, p2.w);
+        const float det = -dot(d, n);
+        const float inv_det = 1.0f / det;
+        const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
+        const V3 dao = cross(ao, d);
+        tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
+        tv = -dot(mk(p0.w, p1.x, p1.y), dao) * inv_det;
+      }
+    } else {
+      const float4 c = a.prims[3 * best];
+      outward = scale(sub(loc, mk(c.x, c.y, c.z)), sh.x);  // (p - c) * (1/r)
+      if (need_uv) {  // sphere.zig:47-51
+        const float theta = dev::acos_z(-outward.y);
+        const float phi = dev::atan2_z(-outward.z, -outward.x) + kPi;
+        tu = phi / kTwoPi;
+        tv = theta / kPi;
+      }
+    }
+    bool front = true;
+    V3 normal = outward;
+    if (dot(d, outward) > 0.0f) {
+      normal = neg(outward);
+      front = false;
+    }
+    // ---- Material.scatter (material.zig:43-129)
+    bool absorbed = false;
+    V3 att = mk(1.0f, 1.0f, 1.0f), nd;
+    if (mkind == ZRT_MAT_LAMBERTIAN) {
+      const float r1 = rand_float(rng);
+      const float r2 = rand_float(rng);
+      const float rr = dev::sqrt_rn(1.0f - r1 * r1);
+      float sn, cs;
+      dev::sincos_z(kTwoPi * r2, &sn, &cs);
+      V3 hv = mk(cs * rr, sn * rr, r1);
+      if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
+      nd = unit(add(normal, hv));
+      att = albedo(mat, a, tu, tv);
+    } else if (mkind == ZRT_MAT_METAL) {
+      nd = unit(reflect(unit(d), normal));
+      if (dot(nd, normal) > 0.0f) att = albedo(mat, a, tu, tv);
+      else absorbed = true;
+    } else {
+      const float ratio = front ? (1.0f / mat.ior()) : mat.ior();
+      const V3 ud = unit(d);
+      const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+      const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
+      bool refl = ratio * sin_theta > 1.0f;
+      if (!refl) {
+        const float r0 = (1.0f - ratio) / (1.0f + ratio);
+        const float reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+        refl = reflectance > rand_float(rng);
+      }
+      nd = unit(refl ? reflect(ud, normal) : refract(ud, normal, ratio));
+    }
+    if (absorbed) {
+      path_end = true;  // black
+    } else {
+      ++c_refl;
+      if (depth_left > 1) {  // an attenuation pushed at depth 1 is never read
+        // every earlier scatter was at a depth > this one, so all were pushed;
+        // the first rows live in LDS, deeper ones in global memory
+        const uint32_t i = a.max_depth - depth_left;
+        if (i < a.att_lds_rows) {
+          att_l[(3 * i + 0) * kBlock] = att.x;
+          att_l[(3 * i + 1) * kBlock] = att.y;
+          att_l[(3 * i + 2) * kBlock] = att.z;
+        } else {
+          a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+        }
+      }
+      o = loc;
+      d = nd;
+      --depth_left;
+    }
+  }
+}
+
 // StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
 // more blocks fit per CU), uint32_t otherwise.
 template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
@@ -1047,8 +1231,16 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   ExcessAcc excess;  // REFERENCE traversal, STATS flavour only
 
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
+  uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0, nodes_prev = 0;  // STATS: SIMD efficiency
   for (;;) {
     ++iters;
+    if (STATS) {  // the wave is converged here: the previous step's traversal trips
+      uint32_t m = c_nodes - nodes_prev;
+      nodes_prev = c_nodes;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+      if (lane == 0) c_trips += m;
+    }
     uint64_t t0 = prof_stamp();
     // ---- work: the WAVE takes units (local tile lt, a group of unit_chunks
     // chunks) from the global counter, one atomic per unit; lane p renders
@@ -1090,6 +1282,10 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       continue;
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[0] += t - t0; t0 = t; }
+    if (STATS) {
+      c_loops += lane == 0 ? 1u : 0u;
+      c_lsteps += runnable ? 1u : 0u;
+    }
     if (!runnable) continue;
 
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
@@ -1149,106 +1345,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph, &excess);
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
-      if (best < 0) {
-        ++c_bg;
-        L = background(d);
-        path_end = true;
-        sky = true;
-      } else {
-        // ---- HitRecord.init (hit_record.zig:28-41)
-        const float4 sh = a.shade[best];
-        const uint32_t tag = __float_as_uint(sh.w);
-        const MatReg mat = load_material(mats, tag & 0x7fffffffu);
-        const uint32_t mkind = mat.kind();
-        const bool need_uv = mkind != ZRT_MAT_DIELECTRIC && mat.tex_kind() == ZRT_TEX_IMAGE;
-        if (STATS) {
-          ++c_shade;
-          c_tex += need_uv ? 1u : 0u;
-        }
-        const V3 loc = add(o, scale(d, best_t));
-        V3 outward;
-        float tu = 0.0f, tv = 0.0f;
-        if (tag >> 31) {
-          outward = mk(sh.x, sh.y, sh.z);  // face_unit_normal
-          if (need_uv) {  // barycentric (u, v), same arithmetic as the hit test
-            const float4 p0 = a.prims[3 * best + 0];
-            const float4 p1 = a.prims[3 * best + 1];
-            const float4 p2 = a.prims[3 * best + 2];
-            const V3 n = mk(p2.y, p2.z, p2.w);
-            const float det = -dot(d, n);
-            const float inv_det = 1.0f / det;
-            const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
-            const V3 dao = cross(ao, d);
-            tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
-            tv = -dot(mk(p0.w, p1.x, p1.y), dao) * inv_det;
-          }
-        } else {
-          const float4 c = a.prims[3 * best];
-          outward = scale(sub(loc, mk(c.x, c.y, c.z)), sh.x);  // (p - c) * (1/r)
-          if (need_uv) {  // sphere.zig:47-51
-            const float theta = dev::acos_z(-outward.y);
-            const float phi = dev::atan2_z(-outward.z, -outward.x) + kPi;
-            tu = phi / kTwoPi;
-            tv = theta / kPi;
-          }
-        }
-        bool front = true;
-        V3 normal = outward;
-        if (dot(d, outward) > 0.0f) {
-          normal = neg(outward);
-          front = false;
-        }
-        // ---- Material.scatter (material.zig:43-129)
-        bool absorbed = false;
-        V3 att = mk(1.0f, 1.0f, 1.0f), nd;
-        if (mkind == ZRT_MAT_LAMBERTIAN) {
-          const float r1 = rand_float(rng);
-          const float r2 = rand_float(rng);
-          const float rr = dev::sqrt_rn(1.0f - r1 * r1);
-          float sn, cs;
-          dev::sincos_z(kTwoPi * r2, &sn, &cs);
-          V3 hv = mk(cs * rr, sn * rr, r1);
-          if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
-          nd = unit(add(normal, hv));
-          att = albedo(mat, a, tu, tv);
-        } else if (mkind == ZRT_MAT_METAL) {
-          nd = unit(reflect(unit(d), normal));
-          if (dot(nd, normal) > 0.0f) att = albedo(mat, a, tu, tv);
-          else absorbed = true;
-        } else {
-          const float ratio = front ? (1.0f / mat.ior()) : mat.ior();
-          const V3 ud = unit(d);
-          const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
-          const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
-          bool refl = ratio * sin_theta > 1.0f;
-          if (!refl) {
-            const float r0 = (1.0f - ratio) / (1.0f + ratio);
-            const float reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
-            refl = reflectance > rand_float(rng);
-          }
-          nd = unit(refl ? reflect(ud, normal) : refract(ud, normal, ratio));
-        }
-        if (absorbed) {
-          path_end = true;  // black
-        } else {
-          ++c_refl;
-          if (depth_left > 1) {  // an attenuation pushed at depth 1 is never read
-            // every earlier scatter was at a depth > this one, so all were pushed;
-            // the first rows live in LDS, deeper ones in global memory
-            const uint32_t i = a.max_depth - depth_left;
-            if (i < a.att_lds_rows) {
-              att_l[(3 * i + 0) * kBlock] = att.x;
-              att_l[(3 * i + 1) * kBlock] = att.y;
-              att_l[(3 * i + 2) * kBlock] = att.z;
-            } else {
-              a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
-            }
-          }
-          o = loc;
-          d = nd;
-          --depth_left;
-        }
-      }
+      shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
+                        c_shade, c_tex);
     }
 
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
@@ -1301,6 +1399,9 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     wave_add_u64(&a.counters[kTexels], c_tex);
     wave_add_u64(&a.counters[kLeaves], c_leaves);
     wave_add_u64(&a.counters[kReplays], c_replays);
+    wave_add_u64(&a.counters[kTravTrips], c_trips);
+    wave_add_u64(&a.counters[kLoopTrips], c_loops);
+    wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
     if (MODE == 2) {
       // maxima of non-negative floats: their bit patterns order like unsigned ints
       uint32_t mt = __float_as_uint(excess.tri), ms = __float_as_uint(excess.sph);
@@ -1318,10 +1419,211 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The wavefront loop (FAST traversal, MODE 4).  render_loop keeps a wave's 64
+// lanes in lockstep: every lane traces one ray per loop step and the wave
+// waits for its slowest traversal.  Where traversal lengths vary a lot between
+// lanes (a large mesh filling the frame: teapot, C5) most lanes idle most of
+// the time (tools/simd_eff.py: 22-29 % traversal lane efficiency on C3/C5 vs
+// 74 % on the bunny).  Here a lane's traversal is suspended between nodes
+// (wide_iter), and the wave alternates two phases, chosen with __ballot:
+//   traverse: node steps for the lanes with a ray in flight, until at least
+//             wf_thresh/64 of the unit's active lanes have finished theirs
+//             (the others stay suspended: node, stack, best hit kept);
+//   shade:    the finished lanes, together, run the rest of their rayColor
+//             step (shade_step) and set up their next ray - the scattered one,
+//             or the camera ray of their pixel's next sample - so they rejoin
+//             the traversal while the suspended lanes go on.
+// The active-ray set is compacted by the ballot counts (no lane waits for the
+// whole wave's traversal), the stacks stay in LDS per lane, and every lane
+// still renders its own pixel's samples in order (sequential chunk sums, the
+// attenuation stack in the recursion's order): images are bit-identical to
+// render_loop's.
+// ---------------------------------------------------------------------------
+template <int PRNG, bool STATS, class StackT>
+__device__ __forceinline__ void render_loop_wf(const KArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
+  float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  float* att_l = reinterpret_cast<float*>(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
+  const DevMaterial* mats = a.mats;
+  if (a.mats_in_lds) {  // block-uniform
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  }
+  const int lane = (int)__lane_id();
+  const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
+
+  bool active = false;     // this lane has samples left in the wave's unit
+  bool in_sample = false;  // ... and one of them is under way
+  bool trav = false;       // ... whose current ray is being traversed
+  uint32_t sample = 0;
+  uint32_t unit_end = 0, chunk_j = 0, x0 = 0, y0 = 0, cur_lt = 0xffffffffu;  // wave-uniform
+  float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
+  V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+  uint32_t depth_left = 0;
+  Rng<PRNG> rng;
+  rng.init(0);
+  // the ray in flight and its suspended traversal
+  RayT r{};
+  float best_t = __builtin_inff();
+  int best = -1;
+  uint32_t sp = 0;
+  const float4* q = nullptr;  // the lane's current node (LDS or global)
+  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
+  uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
+  uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0;  // STATS: SIMD efficiency
+
+  for (;;) {
+    // ---- traverse: node steps while enough lanes still have a ray in flight
+    {
+      const uint32_t n_act = (uint32_t)__builtin_popcountll(__ballot(active));
+      const uint32_t thresh = max(1u, (n_act * a.wf_thresh) >> 6);
+      WideView v{};
+      WideNode w;
+      if (trav) {
+        v = wide_view(a, r, lds_top);
+        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
+      }
+      for (;;) {
+        if (trav) {
+          if (!wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+                                        c_sph)) {
+            wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
+            trav = false;
+          }
+        }
+        if (STATS) c_trips += lane == 0 ? 1u : 0u;
+        if (__ballot(trav) == 0ull) break;
+        if ((uint32_t)__builtin_popcountll(__ballot(active && !trav)) >= thresh) break;
+      }
+    }
+    // ---- refill: the wave's unit is done (lanes wait at unit ends only)
+    if (__ballot(active) == 0ull) {
+      if (a.scanlines && cur_lt != 0xffffffffu) {
+        flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
+        c_depth = c_refl = c_bg = 0;
+      }
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(a.work_counter, 1u);
+      u = __builtin_amdgcn_readfirstlane(u);
+      if (u >= a.total_work) break;  // the counter is exhausted
+      const uint32_t ord = u / a.n_chunks, g = u - ord * a.n_chunks;
+      const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;  // costliest tiles first
+      cur_lt = lt;
+      const uint32_t t = lt * a.world + a.rank;
+      x0 = (t % a.tiles_x) * 8u;
+      y0 = (t / a.tiles_x) * 8u;
+      chunk_j = g;
+      sample = g * a.chunk;
+      unit_end = min(sample + a.chunk, a.spp);
+      active = x0 + ((uint32_t)lane & 7u) < a.xbound && y0 + ((uint32_t)lane >> 3) < a.height;
+      acc_r = acc_g = acc_b = 0.0f;
+      in_sample = false;
+      trav = false;
+    }
+    // ---- shade: the lanes whose ray is done, together
+    if (STATS) {
+      c_loops += lane == 0 ? 1u : 0u;
+      c_lsteps += active && !trav ? 1u : 0u;
+    }
+    if (!active || trav) continue;
+    bool path_end = false, sky = false;
+    V3 L = mk(0.0f, 0.0f, 0.0f);
+    if (in_sample) {
+      shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
+                        c_shade, c_tex);
+      if (!path_end && depth_left == 0) {  // the next rayColor is at depth 0: black (raytrace.zig:64-67)
+        ++c_depth;
+        path_end = true;
+      }
+    }
+    if (path_end) {
+      // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
+      V3 col = L;
+      if (sky) {
+        for (uint32_t i = a.max_depth - depth_left; i-- > 0;) {
+          V3 at;
+          if (i < a.att_lds_rows) {
+            at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
+          } else {
+            const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
+            at = mk(g.x, g.y, g.z);
+          }
+          col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
+        }
+      }
+      acc_r += col.x;
+      acc_g += col.y;
+      acc_b += col.z;
+      in_sample = false;
+      if (++sample == unit_end) {  // chunk done: its sequential sum
+        a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
+        active = false;
+        continue;
+      }
+    }
+    if (!in_sample) {  // a new sample: jitter + Camera.getRay (raytrace.zig:173-175); max_depth >= 1 here
+      const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
+      const uint64_t offset = (uint64_t)py * a.width + px;
+      rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
+      const float u = ((float)px + rand_float(rng) - 0.5f) / a.f_width;
+      const float vv = ((float)py + rand_float(rng) - 0.5f) / a.f_height;
+      const V3 llc = mk(a.llc[0], a.llc[1], a.llc[2]);
+      const V3 hor = mk(a.hor[0], a.hor[1], a.hor[2]);
+      const V3 ver = mk(a.ver[0], a.ver[1], a.ver[2]);
+      o = mk(a.org[0], a.org[1], a.org[2]);
+      d = unit(sub(add(add(llc, scale(hor, u)), scale(ver, vv)), o));
+      depth_left = a.max_depth;
+      in_sample = true;
+    }
+    // ---- the next closest-hit query (raytrace.zig:71-81): suspended at the root
+    if (STATS) ++c_rays;
+    r.ox = o.x; r.oy = o.y; r.oz = o.z;
+    r.dx = d.x; r.dy = d.y; r.dz = d.z;
+    r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+    best_t = __builtin_inff();
+    best = -1;
+    sp = 0;
+    {
+      const WideView v = wide_view(a, r, lds_top);
+      q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+    }
+    trav = true;
+  }
+
+  wave_add_u64(&a.counters[kDepthHits], c_depth);
+  wave_add_u64(&a.counters[kReflections], c_refl);
+  wave_add_u64(&a.counters[kBackground], c_bg);
+  if (STATS) {
+    wave_add_u64(&a.counters[kRays], c_rays);
+    wave_add_u64(&a.counters[kNodes], c_nodes);
+    wave_add_u64(&a.counters[kTriTests], c_tri);
+    wave_add_u64(&a.counters[kSphereTests], c_sph);
+    wave_add_u64(&a.counters[kShades], c_shade);
+    wave_add_u64(&a.counters[kTexels], c_tex);
+    wave_add_u64(&a.counters[kLeaves], c_leaves);
+    wave_add_u64(&a.counters[kReplays], c_replays);
+    wave_add_u64(&a.counters[kTravTrips], c_trips);
+    wave_add_u64(&a.counters[kLoopTrips], c_loops);
+    wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
+  }
+}
+
+#ifndef ZRT_WAVES_WF
+#define ZRT_WAVES_WF 4  // wavefront loop (MODE 4)
+#endif
+
 template <int MODE, int PRNG, bool STATS, class StackT>
-__global__ void __launch_bounds__(kBlock, MODE == 3 ? ZRT_WAVES_WIDE : MODE == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD)
+__global__ void __launch_bounds__(kBlock, MODE == 4   ? ZRT_WAVES_WF
+                                          : MODE == 3 ? ZRT_WAVES_WIDE
+                                          : MODE == 0 ? ZRT_WAVES_LIST
+                                                      : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
-  render_loop<MODE, PRNG, STATS, StackT>(a);
+  if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
+  else render_loop<MODE, PRNG, STATS, StackT>(a);
 }
 
 // The scheduling probe (FAST traversal): the same loop over a few samples per
@@ -1872,6 +2174,19 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->slot_to_prim = h.slot_to_prim;
 }
 
+// The wavefront loop (render_loop_wf) for this scene?  ZRT_WF=0/1 forces it.
+// It doubles the traversal lane efficiency where traversal lengths diverge
+// (C3 0.29 -> 0.59, C5 0.22 -> 0.41), but the FAST loop is bound by its
+// per-lane node fetches (vector memory), not by VALU lane slots, so that buys
+// little time: C5 +2.6 %, C3 -3 .. +1 %, and on the bunny, whose lockstep
+// camera rays share cache lines, it costs a third.  Default:
+// trees too large for the 16-bit stack (million-triangle meshes, C5).
+bool use_wavefront(const zrt_ctx* c, bool stk16) {
+  if (const char* e = std::getenv("ZRT_WF")) return std::atoi(e) != 0;
+  (void)c;
+  return !stk16;
+}
+
 template <int MODE, int PRNG, bool STATS, class StackT>
 void* kernel_ptr() {
   return reinterpret_cast<void*>(&render_kernel<MODE, PRNG, STATS, StackT>);
@@ -1882,6 +2197,7 @@ void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 0) return kernel_ptr<0, PRNG, STATS, uint16_t>();  // list mode: no stack
   if (mode == 1) return stk16 ? kernel_ptr<1, PRNG, STATS, uint16_t>() : kernel_ptr<1, PRNG, STATS, uint32_t>();
   if (mode == 3) return stk16 ? kernel_ptr<3, PRNG, STATS, uint16_t>() : kernel_ptr<3, PRNG, STATS, uint32_t>();
+  if (mode == 4) return stk16 ? kernel_ptr<4, PRNG, STATS, uint16_t>() : kernel_ptr<4, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
 void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
@@ -2242,7 +2558,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
                                        size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
                                  : c->n_nodes < 65536;
-    void* kfn = zrt::select_kernel(mode, p->prng, diag, stk16);
+    // FAST: the wavefront loop (MODE 4) where lanes' traversal lengths diverge
+    const bool wf = mode == 3 && p->max_depth >= 1 && zrt::use_wavefront(c, stk16);
+    void* kfn = zrt::select_kernel(wf ? 4 : mode, p->prng, diag, stk16);
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
@@ -2331,6 +2649,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                    lp.mats_in_lds ? c->n_mats : 0u, lp.mat_off);
     a.chunk = chunk;
     a.n_chunks = n_chunks;
+    a.wf_thresh = 32;  // shade once half of the unit's active lanes are ready
+    if (const char* e = std::getenv("ZRT_WF_THRESH")) a.wf_thresh = std::max(1, std::min(64, std::atoi(e)));
     a.sync = ZRT_SYNC_SAMPLES;
     if (const char* e = std::getenv("ZRT_SYNC"))  // A/B: lockstep interval in samples (identical images)
       a.sync = std::max(1u, uint32_t(std::atoi(e)));
