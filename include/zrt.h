@@ -431,6 +431,15 @@ typedef struct zrt_bvh_node {
 int zrt_bvh_build(const zrt_scene* scene, zrt_bvh_node** out_nodes,
                   uint32_t* n_nodes, uint32_t* max_depth);
 
+/* The same tree built on GPU `device` (bvh.zig:62-185 level by level: each
+ * level's stable axis sorts as segmented radix sorts, the split scores as
+ * one wave per segment).  Node for node equal to zrt_bvh_build.
+ * The context entry points use it for scenes of >= 65536 primitives.
+ * ZRT_E_UNSUPPORTED for < 3 primitives or NaN midpoints (the host build
+ * handles those). */
+int zrt_bvh_build_device(const zrt_scene* scene, uint32_t device, zrt_bvh_node** out_nodes,
+                         uint32_t* n_nodes, uint32_t* max_depth);
+
 /* ---- device parity probes ------------------------------------------------ *
  * Evaluate the kernel's own device functions on inputs, for bit-exact
  * comparison with the oracle's restatements:

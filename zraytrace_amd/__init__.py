@@ -302,6 +302,19 @@ def bvh_build(scene):
         lib().zrt_free(C.cast(nodes, C.c_void_p))
 
 
+def bvh_build_device(scene, device: int = 0):
+    """The same BVH built on the GPU (zrt_bvh_build_device), as bvh_build returns it."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    nodes = C.POINTER(_ffi.BvhNode)()
+    n = C.c_uint32()
+    depth = C.c_uint32()
+    check(lib().zrt_bvh_build_device(view, device, C.byref(nodes), C.byref(n), C.byref(depth)))
+    try:
+        return nodes_to_numpy(nodes, n.value) + (depth.value,)
+    finally:
+        lib().zrt_free(C.cast(nodes, C.c_void_p))
+
+
 def nodes_to_numpy(nodes, n):
     dt = np.dtype([("min", "<f4", 3), ("left", "<i4"), ("max", "<f4", 3), ("right", "<i4")])
     buf = np.ctypeslib.as_array(C.cast(nodes, C.POINTER(C.c_uint8)), shape=(n * 32,)).copy()

@@ -162,6 +162,8 @@ SIGNATURES = [
     ("zrt_image_write_ppm", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
     ("zrt_bvh_build", C.c_int, [C.POINTER(Scene), C.POINTER(C.POINTER(BvhNode)),
                                 C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("zrt_bvh_build_device", C.c_int, [C.POINTER(Scene), C.c_uint32, C.POINTER(C.POINTER(BvhNode)),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     ("zrt_debug_math", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float), C.c_uint32, C.c_uint32]),
     ("zrt_debug_rng", C.c_int, [C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64),

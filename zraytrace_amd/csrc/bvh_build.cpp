@@ -34,14 +34,8 @@
 
 namespace zrt {
 
-namespace {
-
 inline float fmin_z(float x, float y) { return x < y ? x : y; }  // std.math.min
 inline float fmax_z(float x, float y) { return x > y ? x : y; }  // std.math.max
-
-struct Box {
-  float mn[3], mx[3], mid[3];
-};
 
 // aabb.zig:37-41 initMinMax
 Box box_min_max(const float c1[3], const float c2[3]) {
@@ -84,6 +78,15 @@ Box prim_box(const zrt_prim& p) {
   return box_union(box_min_max(a, b), box_min_max(a, c));
 }
 
+uint32_t mid_key(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if (f == 0.0f) u = 0;  // -0 == +0 under `<`
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+namespace {
+
 struct Builder {
   const std::vector<Box>& pbox;
   std::vector<uint32_t>& order;  // the slice being divided, permuted in place
@@ -123,11 +126,7 @@ struct Builder {
     idx_b.resize(n);
     uint32_t* idx_a = order.data() + lo;
     for (size_t i = 0; i < n; ++i) {
-      const float f = pb[idx_a[i]].mid[axis];
-      uint32_t u;
-      std::memcpy(&u, &f, 4);
-      if (f == 0.0f) u = 0;  // -0 == +0 under `<`
-      key_a[i] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      key_a[i] = mid_key(pb[idx_a[i]].mid[axis]);
     }
     uint32_t *ka = key_a.data(), *kb = key_b.data(), *ia = idx_a, *ib = idx_b.data();
     for (int shift = 0; shift < 32; shift += 8) {

@@ -1960,15 +1960,28 @@ struct HostScene {
   double preprocess_ms = 0;
 };
 
+// Meshes from this many primitives have their reference BVH built on the GPU
+// (bvh_gpu.hip: same tree; 1.6 M triangles in a fraction of a second instead of
+// 5.6 s on the host).  ZRT_BVH_DEVICE=0/1 forces the host / device build.
+constexpr uint32_t kDeviceBvhMin = 1u << 16;
+bool device_bvh(uint32_t n) {
+  if (const char* e = std::getenv("ZRT_BVH_DEVICE")) return std::atoi(e) != 0;
+  return n >= kDeviceBvhMin;
+}
+
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
-void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
+// `device` >= 0: the GPU that may build the BVH (device_bvh).
+void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
   std::vector<uint32_t> slot_to_prim, leaf_of_slot;
   std::vector<float4> nodes;
   uint32_t depth = 0;
   if (use_bvh) {
-    const BuiltBvh bvh = build_bvh(s->prims, n);
+    BuiltBvh bvh;
+    if (!(device >= 0 && device_bvh(n) && build_bvh_device(s->prims, n, device, &bvh))) bvh = build_bvh(s->prims, n);
+    if (std::getenv("ZRT_DEBUG_LAUNCH"))
+      std::fprintf(stderr, "zrt preprocess: reference BVH %zu nodes in %.1f ms\n", bvh.nodes.size(), now_ms() - t0);
     depth = bvh.max_depth;
     nodes.resize(2 * bvh.nodes.size());
     std::vector<int32_t> prim_slot(n, -1);
@@ -2011,7 +2024,10 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh) {
       nodes[2 * i + 1] = hi;
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
+    const double tw = now_ms();
     const WideBvh wide = build_wide_bvh(leaves);
+    if (std::getenv("ZRT_DEBUG_LAUNCH"))
+      std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
 #if ZRT_OCT_COPIES
     // one copy per ray octant o (bit k set: direction k negative) with axis k's
@@ -2495,7 +2511,7 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
     // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
     zrt::HostScene h;
-    zrt::flatten_scene(&h, scene, use_bvh);
+    zrt::flatten_scene(&h, scene, use_bvh, int(params->device));
     *out = zrt::ctx_on_device(h, int(params->device)).release();
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
@@ -2649,7 +2665,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                    lp.mats_in_lds ? c->n_mats : 0u, lp.mat_off);
     a.chunk = chunk;
     a.n_chunks = n_chunks;
-    a.wf_thresh = 32;  // shade once half of the unit's active lanes are ready
+    a.wf_thresh = 48;  // shade once 3/4 of the unit's active lanes are ready (C5: 32 -> 7.32, 48 -> 7.71, 56 -> 7.70 Gray/s)
     if (const char* e = std::getenv("ZRT_WF_THRESH")) a.wf_thresh = std::max(1, std::min(64, std::atoi(e)));
     a.sync = ZRT_SYNC_SAMPLES;
     if (const char* e = std::getenv("ZRT_SYNC"))  // A/B: lockstep interval in samples (identical images)
@@ -2972,7 +2988,7 @@ int zrt_multi_create(const zrt_scene* scene, const zrt_params* params, const uin
     // the scene flattened once (BVH build, raytrace.zig:124-133), a copy on every GPU
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
     zrt::HostScene host;
-    zrt::flatten_scene(&host, scene, use_bvh);
+    zrt::flatten_scene(&host, scene, use_bvh, int(devices[0]));
     for (uint32_t r = 0; r < n_devices; ++r) m->ctx.emplace_back(zrt::ctx_on_device(host, int(devices[r])).release());
     m->send.resize(n_devices);
     if (m->use_rccl) {
@@ -3141,7 +3157,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
   try {
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
     zrt::HostScene h;
-    zrt::flatten_scene(&h, scene, use_bvh);
+    zrt::flatten_scene(&h, scene, use_bvh, int(params->device));
     std::unique_ptr<zrt_ctx> c = zrt::ctx_on_device(h, int(params->device));
     const int mode = !c->use_bvh ? 0
                      : params->traversal == ZRT_TRAVERSAL_REFERENCE ? 2
