@@ -361,7 +361,7 @@ int zrt_ctx_assemble_padded(zrt_ctx* ctx, const zrt_params* params,
 /* Counters of the last zrt_ctx_render_tiles (waits for that launch). */
 int zrt_ctx_stats(zrt_ctx* ctx, zrt_stats* out);
 
-/* Raw device counter slots of the last launch (diagnostics; n <= 24):
+/* Raw device counter slots of the last launch (diagnostics; n <= 32):
  * [0..9] progress/traffic counters, [14] work counter, [15] error flag,
  * [16..20] per-section cycle sums of ZRT_PROFILE builds. */
 int zrt_ctx_debug_counters(zrt_ctx* ctx, uint64_t* out, uint32_t n);

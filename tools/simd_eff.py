@@ -21,13 +21,17 @@ for spec in sys.argv[1:] or ["2:2048:2048:16", "3:1024:1024:16", "6:4096:4096:4"
     buf = torch.zeros(ctx.tile_count(p) * 64 * 3, dtype=torch.float32, device="cuda")
     ctx.render_tiles(s.camera, p, buf.data_ptr())
     st = ctx.stats()
-    c = ctx.debug_counters(24)
+    c = ctx.debug_counters(32)
     trips, loops, lsteps = c[21], c[22], c[23]
     out = {"scene": sc, "width": w, "height": h, "spp": spp, "rays": st["rays_processed"],
            "node_visits": st["node_visits"], "trav_trips": trips, "loop_trips": loops, "lane_steps": lsteps,
            "trav_lane_eff": round(st["node_visits"] / max(1, 64 * trips), 4),
            "step_lane_eff": round(lsteps / max(1, 64 * loops), 4),
            "nodes_per_ray": round(st["node_visits"] / st["rays_processed"], 3),
-           "trips_per_loop": round(trips / max(1, loops), 3), "kernel_ms": st["render_ms"]}
+           "trips_per_loop": round(trips / max(1, loops), 3), "kernel_ms": st["render_ms"],
+           "global_nodes_per_ray": round(c[24] / st["rays_processed"], 3),
+           "uniform_node_frac": round(c[25] / max(1, c[24]), 4),
+           "prim_tests_per_ray": round(c[26] / st["rays_processed"], 3),
+           "uniform_prim_frac": round(c[27] / max(1, c[26]), 4)}
     print(json.dumps(out), flush=True)
     ctx.close()

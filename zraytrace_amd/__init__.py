@@ -251,7 +251,7 @@ class RenderContext:
         check(lib().zrt_ctx_stats(self._h, C.byref(st)))
         return st.as_dict()
 
-    def debug_counters(self, n: int = 24):
+    def debug_counters(self, n: int = 32):
         out = (C.c_uint64 * n)()
         check(lib().zrt_ctx_debug_counters(self._h, out, n))
         return list(out)

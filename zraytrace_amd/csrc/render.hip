@@ -108,12 +108,18 @@ struct KArgs {
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
        kLeaves, kReplays, kExcessTri, kExcessSph, kExcessHits, kNumCounters };
-constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 24;
+constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 32;
 // STATS flavour, SIMD efficiency (zrt_ctx_debug_counters): traversal loop trips
 // of the waves (per traced step, the most node visits of any lane: kNodes /
 // (64 kTravTrips) is the lane efficiency of traversal), loop iterations in which
 // some lane ran a rayColor step, and the lane-steps run in them
 constexpr int kTravTrips = 21, kLoopTrips = 22, kLaneSteps = 23;
+// STATS flavour, coherence of the FAST loop's vector-memory fetches (lane
+// counts): wide nodes read from global memory, and those read while every
+// active lane of the wave read the same node; primitive tests, and those in
+// which every active lane tested the same primitive (a wave-uniform address
+// could come through the scalar cache instead of the vector data return)
+constexpr int kGlobalNodes = 24, kUniformNodes = 25, kPrimLaneTests = 26, kUniformPrims = 27;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
 // cycle sums per loop section into counters[kProfSlot + section].
@@ -402,6 +408,38 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
   } else {
     if (STATS) ++c_sph;
     sphere_test<TIE, TRACK>(prims[3 * slot], slot, r, best_t, best, leafp);
+  }
+}
+
+#ifndef ZRT_SCALAR_NODES
+#define ZRT_SCALAR_NODES 1  // FAST: a wide node every active lane reads next comes through the scalar cache
+#endif
+#ifndef ZRT_SCALAR_PRIMS
+#define ZRT_SCALAR_PRIMS 1  // FAST: a primitive every active lane tests is read through the scalar cache
+#endif
+// prim_test for a WAVE-UNIFORM ref: the record is read with scalar loads
+// (s_load through the constant address space), so the 48 bytes do not cross
+// the vector data return (TD), which is what the FAST loop saturates (DESIGN.md
+// §4); on the bunny 89 % of the leaf trips test one primitive in every active
+// lane (tools/simd_eff.py uniform_prim_frac).  Same arithmetic as prim_test.
+template <bool TIE, bool STATS, bool TRACK = false>
+__device__ __forceinline__ void prim_test_uniform(const float4* __restrict__ prims, int ref, const RayT& r,
+                                                  float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph,
+                                                  const float* leafp = nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) float4 cfloat4;
+  cfloat4* cp = (cfloat4*)prims;
+#else
+  const float4* cp = prims;
+#endif
+  const int code = -ref - 1;
+  const int slot = code >> 1;
+  if (code & 1) {
+    if (STATS) ++c_tri;
+    tri_test_v<TIE, TRACK>(cp[3 * slot + 0], cp[3 * slot + 1], cp[3 * slot + 2], slot, r, best_t, best, leafp);
+  } else {
+    if (STATS) ++c_sph;
+    sphere_test<TIE, TRACK>(cp[3 * slot], slot, r, best_t, best, leafp);
   }
 }
 
@@ -734,6 +772,12 @@ __device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict
 // test still uses the current best with lower-slot tie-breaking); leaf slots
 // are intersected in place, inner slots are sorted by entry distance and the
 // farther ones pushed, branch-free.
+// STATS: coherence of the FAST loop's fetches (kGlobalNodes .. kUniformPrims)
+struct Coh {
+  uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0;
+  __device__ __forceinline__ void flush(unsigned long long* counters);
+};
+
 // One wide node's record in registers: the four slots' near planes, far planes
 // (per axis, pre-swapped in the ray's octant copy) and primitive/child refs.
 struct WideNode {
@@ -802,11 +846,12 @@ __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const Wid
 // the order-hazard test of wide_finish follows).  Its state between calls is
 // (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
-template <bool STATS, class StackT>
+template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
                                           const float4*& q, uint32_t& sp, float& best_t, int& best,
-                                          uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph) {
+                                          uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
+                                          Coh& coh) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
   // the first rows in LDS, the rest in global memory (32-bit stacks only: the
@@ -906,8 +951,19 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         const int L = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
         const int pb = as_int(k == 0 ? rb.x : k == 1 ? rb.y : k == 2 ? rb.z : rb.w);
         const float* lp = ZRT_HAZARD_ENTRY ? reinterpret_cast<const float*>(leaf_q) + k : nullptr;
-        prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);
-        if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
+        if (STATS) {
+          const int f = __builtin_amdgcn_readfirstlane(L);
+          coh.ptests += 1u;
+          coh.uprims += __ballot(L != f) == 0ull ? 1u : 0u;
+        }
+        const int fl = __builtin_amdgcn_readfirstlane(L), fb = __builtin_amdgcn_readfirstlane(pb);
+        if (ZRT_SCALAR_PRIMS && __ballot(L != fl || pb != fb) == 0ull) {  // one leaf in every active lane
+          prim_test_uniform<true, STATS, ZRT_ORDER_EXACT>(a.prims, fl, r, best_t, best, c_tri, c_sph, lp);
+          if (fb != fl) prim_test_uniform<true, STATS, ZRT_ORDER_EXACT>(a.prims, fb, r, best_t, best, c_tri, c_sph, lp);
+        } else {
+          prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);
+          if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
+        }
       } while (open != 0);
     }
   } else if ((l0 | l1 | l2 | l3) != 0) {
@@ -925,15 +981,32 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     ZRT_WIDE_LEAF(l3, rb.w, 3)
 #undef ZRT_WIDE_LEAF
   }
+  if (STATS && next >= 0 && (uint32_t)next >= v.n_top) {
+    const int32_t f = __builtin_amdgcn_readfirstlane(next);
+    const bool uni = __ballot(next != f || (uint32_t)next < v.n_top) == 0ull;  // (among the lanes here)
+    ++coh.gnodes;
+    coh.unodes += uni ? 1u : 0u;
+  }
   if (next < 0) return false;
   if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS (ds_read)
     const float4* __restrict__ t = v.top + 8u * (uint32_t)next;
     q = t;
     wide_load(t, sx, sy, sz, w);
   } else {
-    const float4* __restrict__ g = a.wnodes + (v.base + 8u * (uint32_t)next);
+    const uint32_t at = v.base + 8u * (uint32_t)next;  // this ray's octant copy
+    const float4* __restrict__ g = a.wnodes + at;
     q = g;
-    wide_load(g, sx, sy, sz, w);
+    const uint32_t fa = __builtin_amdgcn_readfirstlane(at);
+    if (SCALAR_NODES && __ballot(at != fa) == 0ull) {  // one node in every active lane: scalar loads
+#if defined(__HIP_DEVICE_COMPILE__)
+      typedef const __attribute__((address_space(4))) float4 cfloat4;
+      wide_load(reinterpret_cast<const float4*>((cfloat4*)a.wnodes + fa), sx, sy, sz, w);
+#else
+      wide_load(a.wnodes + fa, sx, sy, sz, w);
+#endif
+    } else {
+      wide_load(g, sx, sy, sz, w);
+    }
   }
   return true;
 }
@@ -957,14 +1030,14 @@ template <bool STATS, class StackT>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                               const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
                                               int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
-                                              uint32_t& c_sph, uint32_t& c_replays) {
+                                              uint32_t& c_sph, uint32_t& c_replays, Coh& coh) {
   const WideView v = wide_view(a, r, lds_top);
   uint32_t sp = 0;
   // the root is node 0 of this octant's copy (in LDS when the top levels are)
   const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
   WideNode w;
   wide_load(q, v.sx, v.sy, v.sz, w);
-  while (wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph)) {
+  while (wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
@@ -1050,6 +1123,13 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
   if (__lane_id() == 0 && (lo | hi)) atomicAdd(dst, ((unsigned long long)hi << 32) | lo);
 }
 
+__device__ __forceinline__ void Coh::flush(unsigned long long* counters) {
+  wave_add_u64(&counters[kGlobalNodes], gnodes);
+  wave_add_u64(&counters[kUniformNodes], unodes);
+  wave_add_u64(&counters[kPrimLaneTests], ptests);
+  wave_add_u64(&counters[kUniformPrims], uprims);
+}
+
 // ZRT_FLAG_SCANLINES: a finished unit's counters added to its frame rows.  The
 // 8 lanes of a tile row (lanes 8k .. 8k+7) are summed with shuffles, then one
 // lane per row adds them.  Called with the whole wave converged.
@@ -1101,7 +1181,18 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
     sky = true;
   } else {
     // ---- HitRecord.init (hit_record.zig:28-41)
-    const float4 sh = a.shade[best];
+    float4 sh;
+    const int fb = __builtin_amdgcn_readfirstlane(best);
+    if (ZRT_SCALAR_PRIMS && __ballot(best != fb) == 0ull) {  // one hit surface in every lane here
+#if defined(__HIP_DEVICE_COMPILE__)
+      typedef const __attribute__((address_space(4))) float4 cfloat4;
+      sh = ((cfloat4*)a.shade)[fb];
+#else
+      sh = a.shade[fb];
+#endif
+    } else {
+      sh = a.shade[best];
+    }
     const uint32_t tag = __float_as_uint(sh.w);
     const MatReg mat = load_material(mats, tag & 0x7fffffffu);
     const uint32_t mkind = mat.kind();
@@ -1228,6 +1319,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   rng.init(0);
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
+  Coh coh;  // STATS
   ExcessAcc excess;  // REFERENCE traversal, STATS flavour only
 
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
@@ -1340,7 +1432,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
-        traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
+        traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph, &excess);
       }
@@ -1402,6 +1494,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     wave_add_u64(&a.counters[kTravTrips], c_trips);
     wave_add_u64(&a.counters[kLoopTrips], c_loops);
     wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
+    coh.flush(a.counters);
     if (MODE == 2) {
       // maxima of non-negative floats: their bit patterns order like unsigned ints
       uint32_t mt = __float_as_uint(excess.tri), ms = __float_as_uint(excess.sph);
@@ -1474,6 +1567,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   const float4* q = nullptr;  // the lane's current node (LDS or global)
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
+  Coh coh;  // STATS
   uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0;  // STATS: SIMD efficiency
 
   for (;;) {
@@ -1489,8 +1583,9 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       }
       for (;;) {
         if (trav) {
-          if (!wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
-                                        c_sph)) {
+          // (its lanes' nodes are rarely one: no scalar-load test, C5 -1.4 % with it)
+          if (!wide_iter<STATS, StackT, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+                                               c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             trav = false;
           }
@@ -1609,6 +1704,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     wave_add_u64(&a.counters[kTravTrips], c_trips);
     wave_add_u64(&a.counters[kLoopTrips], c_loops);
     wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
+    coh.flush(a.counters);
   }
 }
 
@@ -1663,7 +1759,8 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
     }
   } else if (MODE == 3) {
     uint32_t c_replays = 0;
-    traverse_wide<false>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays);
+    Coh coh;
+    traverse_wide<false>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
   } else {
     traverse_bvh<MODE == 1, false>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
   }
