@@ -12,6 +12,12 @@ import torch  # noqa: E402
 
 import zraytrace_amd as z  # noqa: E402
 
+def ctx_units(ctx, p):
+    """Work units (tile x sample chunk) of the launch: each writes 64 chunk sums of 16 B."""
+    chunk = p.sample_chunk or 32
+    return ctx.tile_count(p) * ((p.samples_per_pixel + chunk - 1) // chunk)
+
+
 for spec in sys.argv[1:] or ["2:2048:2048:16", "3:1024:1024:16", "6:4096:4096:4"]:
     sc, w, h, spp = (int(v) for v in spec.split(":"))
     s = z.load_scene(sc)
@@ -32,6 +38,8 @@ for spec in sys.argv[1:] or ["2:2048:2048:16", "3:1024:1024:16", "6:4096:4096:4"
            "global_nodes_per_ray": round(c[24] / st["rays_processed"], 3),
            "uniform_node_frac": round(c[25] / max(1, c[24]), 4),
            "prim_tests_per_ray": round(c[26] / st["rays_processed"], 3),
-           "uniform_prim_frac": round(c[27] / max(1, c[26]), 4)}
+           "uniform_prim_frac": round(c[27] / max(1, c[26]), 4),
+           "att_global_writes": c[28], "att_global_reads": c[29], "units": ctx_units(ctx, p),
+           "chunk_sum_bytes": 16 * 64 * ctx_units(ctx, p)}
     print(json.dumps(out), flush=True)
     ctx.close()

@@ -65,17 +65,30 @@ class RenderParams:
 
 
 class LoadedScene:
-    """A scene of scenes.zig built by the C++ host mirror (zrt_scene_load)."""
+    """A scene of scenes.zig built by the C++ host mirror (zrt_scene_load), or
+    read back from a binary scene file (zrt_scene_read, LoadedScene.read)."""
 
-    def __init__(self, index: int, assets_dir: str = ASSETS):
+    def __init__(self, index: int, assets_dir: str = ASSETS, _path: str = None):
         L = lib()
         h = C.c_void_p()
         cam = _ffi.Camera()
-        check(L.zrt_scene_load(index, assets_dir.encode(), C.byref(h), C.byref(cam)))
+        if _path is None:
+            check(L.zrt_scene_load(index, assets_dir.encode(), C.byref(h), C.byref(cam)))
+        else:
+            check(L.zrt_scene_read(_path.encode(), C.byref(h), C.byref(cam)))
         self._h = h
         self.index = index
         self.camera = cam
         self.view = L.zrt_scene_view(h)  # POINTER(Scene)
+
+    @classmethod
+    def read(cls, path: str) -> "LoadedScene":
+        """A scene written by write() (zrt_scene_read)."""
+        return cls(-1, _path=path)
+
+    def write(self, path: str):
+        """The flat scene and its camera as a binary scene file (zrt_scene_write)."""
+        check(lib().zrt_scene_write(self.view, C.byref(self.camera), path.encode()))
 
     @property
     def n_prims(self) -> int:

@@ -153,6 +153,8 @@ SIGNATURES = [
     ("zrt_scene_load", C.c_int, [C.c_uint32, C.c_char_p, C.POINTER(_P), C.POINTER(Camera)]),
     ("zrt_scene_view", C.POINTER(Scene), [_P]),
     ("zrt_scene_free", None, [_P]),
+    ("zrt_scene_write", C.c_int, [C.POINTER(Scene), C.POINTER(Camera), C.c_char_p]),
+    ("zrt_scene_read", C.c_int, [C.c_char_p, C.POINTER(_P), C.POINTER(Camera)]),
     ("zrt_obj_read", C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.POINTER(Prim)),
                                C.POINTER(C.c_uint32)]),
     ("zrt_free", None, [_P]),

@@ -120,6 +120,9 @@ constexpr int kTravTrips = 21, kLoopTrips = 22, kLaneSteps = 23;
 // which every active lane tested the same primitive (a wave-uniform address
 // could come through the scalar cache instead of the vector data return)
 constexpr int kGlobalNodes = 24, kUniformNodes = 25, kPrimLaneTests = 26, kUniformPrims = 27;
+// STATS: attenuation-stack rows written to / read from global memory (rows past
+// the LDS ones): with the chunk sums, the loop's HBM writes
+constexpr int kAttWrites = 28, kAttReads = 29;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
 // cycle sums per loop section into counters[kProfSlot + section].
@@ -774,7 +777,7 @@ __device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict
 // farther ones pushed, branch-free.
 // STATS: coherence of the FAST loop's fetches (kGlobalNodes .. kUniformPrims)
 struct Coh {
-  uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0;
+  uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0, attw = 0, attr = 0;
   __device__ __forceinline__ void flush(unsigned long long* counters);
 };
 
@@ -1128,6 +1131,8 @@ __device__ __forceinline__ void Coh::flush(unsigned long long* counters) {
   wave_add_u64(&counters[kUniformNodes], unodes);
   wave_add_u64(&counters[kPrimLaneTests], ptests);
   wave_add_u64(&counters[kUniformPrims], uprims);
+  wave_add_u64(&counters[kAttWrites], attw);
+  wave_add_u64(&counters[kAttReads], attr);
 }
 
 // ZRT_FLAG_SCANLINES: a finished unit's counters added to its frame rows.  The
@@ -1173,7 +1178,8 @@ template <bool STATS, class R>
 __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __restrict__ mats,
                                            float* __restrict__ att_l, uint32_t gl, R& rng, int best, float best_t,
                                            V3& o, V3& d, uint32_t& depth_left, bool& path_end, bool& sky, V3& L,
-                                           uint32_t& c_bg, uint32_t& c_refl, uint32_t& c_shade, uint32_t& c_tex) {
+                                           uint32_t& c_bg, uint32_t& c_refl, uint32_t& c_shade, uint32_t& c_tex,
+                                           Coh& coh) {
   if (best < 0) {
     ++c_bg;
     L = background(d);
@@ -1278,6 +1284,7 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
           att_l[(3 * i + 2) * kBlock] = att.z;
         } else {
           a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+          if (STATS) ++coh.attw;
         }
       }
       o = loc;
@@ -1438,7 +1445,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
       shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
-                        c_shade, c_tex);
+                        c_shade, c_tex, coh);
     }
 
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
@@ -1454,6 +1461,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
             at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
           } else {
             const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
+            if (STATS) ++coh.attr;
             at = mk(g.x, g.y, g.z);
           }
           col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
@@ -1629,7 +1637,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     V3 L = mk(0.0f, 0.0f, 0.0f);
     if (in_sample) {
       shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
-                        c_shade, c_tex);
+                        c_shade, c_tex, coh);
       if (!path_end && depth_left == 0) {  // the next rayColor is at depth 0: black (raytrace.zig:64-67)
         ++c_depth;
         path_end = true;
@@ -1645,6 +1653,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
             at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
           } else {
             const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
+            if (STATS) ++coh.attr;
             at = mk(g.x, g.y, g.z);
           }
           col = mk(at.x * col.x, at.y * col.y, at.z * col.z);

@@ -550,6 +550,106 @@ const zrt_scene* zrt_scene_view(const zrt_scene_data* data) {
 
 void zrt_scene_free(zrt_scene_data* data) { delete data; }
 
+// ---- binary scene files (the C5 mesh without re-parsing and subdividing) ----
+// Layout (little endian): "ZRTS", u32 version, u32 sizeof(zrt_prim),
+// sizeof(zrt_material), sizeof(zrt_texture), u32 n_prims, n_materials,
+// n_textures, n_images, the camera (12 f32), then the flat arrays as zrt.h
+// lays them out and each image as u32 width, height + width*height*3 f32.
+namespace {
+constexpr uint32_t kSceneFileVersion = 1;
+
+struct File {
+  FILE* f;
+  explicit File(FILE* f_) : f(f_) {}
+  ~File() {
+    if (f) std::fclose(f);
+  }
+};
+
+void put(FILE* f, const void* p, size_t n) {
+  if (n && std::fwrite(p, 1, n, f) != n) throw zrt::Error(ZRT_E_IO, "short write");
+}
+void get(FILE* f, void* p, size_t n) {
+  if (n && std::fread(p, 1, n, f) != n) throw zrt::Error(ZRT_E_IO, "truncated scene file");
+}
+}  // namespace
+
+int zrt_scene_write(const zrt_scene* scene, const zrt_camera* camera, const char* path) {
+  if (!scene || !camera || !path) return zrt::fail(ZRT_E_INVALID, "null argument");
+  if ((scene->n_prims && !scene->prims) || (scene->n_materials && !scene->materials) ||
+      (scene->n_textures && !scene->textures) || (scene->n_images && !scene->images))
+    return zrt::fail(ZRT_E_INVALID, "scene array is null with a non-zero count");
+  try {
+    File out(std::fopen(path, "wb"));
+    if (!out.f) return zrt::fail(ZRT_E_IO, std::string("cannot open ") + path);
+    const uint32_t head[9] = {kSceneFileVersion, uint32_t(sizeof(zrt_prim)), uint32_t(sizeof(zrt_material)),
+                              uint32_t(sizeof(zrt_texture)), scene->n_prims, scene->n_materials,
+                              scene->n_textures, scene->n_images, 0};
+    put(out.f, "ZRTS", 4);
+    put(out.f, head, sizeof(head));
+    put(out.f, camera, sizeof(zrt_camera));
+    put(out.f, scene->prims, sizeof(zrt_prim) * size_t(scene->n_prims));
+    put(out.f, scene->materials, sizeof(zrt_material) * size_t(scene->n_materials));
+    put(out.f, scene->textures, sizeof(zrt_texture) * size_t(scene->n_textures));
+    for (uint32_t i = 0; i < scene->n_images; ++i) {
+      const zrt_image& im = scene->images[i];
+      const uint32_t wh[2] = {im.width, im.height};
+      put(out.f, wh, sizeof(wh));
+      put(out.f, im.pixels, sizeof(float) * 3 * size_t(im.width) * im.height);
+    }
+    if (std::fflush(out.f) != 0) return zrt::fail(ZRT_E_IO, "write failed");
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  }
+}
+
+int zrt_scene_read(const char* path, zrt_scene_data** out, zrt_camera* camera) {
+  if (!path || !out) return zrt::fail(ZRT_E_INVALID, "null argument");
+  *out = nullptr;
+  try {
+    File in(std::fopen(path, "rb"));
+    if (!in.f) return zrt::fail(ZRT_E_IO, std::string("cannot open ") + path);
+    char magic[4];
+    uint32_t head[9];
+    get(in.f, magic, 4);
+    get(in.f, head, sizeof(head));
+    if (std::memcmp(magic, "ZRTS", 4) != 0 || head[0] != kSceneFileVersion || head[1] != sizeof(zrt_prim) ||
+        head[2] != sizeof(zrt_material) || head[3] != sizeof(zrt_texture))
+      return zrt::fail(ZRT_E_PARSE, std::string(path) + ": not a version-1 zrt scene file");
+    std::unique_ptr<zrt_scene_data> h(new zrt_scene_data);
+    h->sd.reset(new zrt::SceneData);
+    zrt::FlatScene& fs = h->sd->flat;
+    zrt_camera cam;
+    get(in.f, &cam, sizeof(cam));
+    fs.prims.resize(head[4]);
+    fs.materials.resize(head[5]);
+    fs.textures.resize(head[6]);
+    get(in.f, fs.prims.data(), sizeof(zrt_prim) * fs.prims.size());
+    get(in.f, fs.materials.data(), sizeof(zrt_material) * fs.materials.size());
+    get(in.f, fs.textures.data(), sizeof(zrt_texture) * fs.textures.size());
+    for (uint32_t i = 0; i < head[7]; ++i) {
+      uint32_t wh[2];
+      get(in.f, wh, sizeof(wh));
+      if (uint64_t(wh[0]) * wh[1] > (1ull << 30)) return zrt::fail(ZRT_E_PARSE, "image too large");
+      auto img = zrt::Image::init(wh[0], wh[1]);
+      get(in.f, img->pixels.data(), sizeof(float) * img->pixels.size());
+      fs.images.push_back(zrt_image{wh[0], wh[1], img->pixels.data()});
+      h->sd->images.push_back(std::move(img));
+    }
+    for (const zrt_prim& p : fs.prims)
+      if (p.material >= fs.materials.size()) return zrt::fail(ZRT_E_PARSE, "primitive material out of range");
+    fs.finalize();
+    if (camera) *camera = cam;
+    *out = h.release();
+    return ZRT_OK;
+  } catch (const zrt::Error& e) {
+    return zrt::fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return zrt::fail(ZRT_E_NOMEM, "OutOfMemory");
+  }
+}
+
 int zrt_obj_read(const char* path, uint32_t material, zrt_prim** out_prims, uint32_t* n_prims) {
   if (!path || !out_prims || !n_prims) return zrt::fail(ZRT_E_INVALID, "null argument");
   *out_prims = nullptr;
