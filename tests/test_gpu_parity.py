@@ -104,6 +104,24 @@ def test_render_bit_exact_vs_oracle(scenes, case, traversal):
         assert gs["node_visits"] == rs["node_visits"]
 
 
+@pytest.mark.parametrize("loop", ["lockstep", "wavefront"])
+@pytest.mark.parametrize("case", [c for c in CASES if c[0] != 1], ids=[f"scene{c[0]}" for c in CASES if c[0] != 1])
+def test_render_loops_bit_exact(scenes, case, loop, monkeypatch):
+    """Both FAST sampling loops (render_loop and the wavefront render_loop_wf,
+    DESIGN.md §3) on every BVH scene, with more samples per pixel and a chunk that
+    splits them: images, counters and per-scanline counters equal the oracle's."""
+    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    idx, w, h, _, depth = case
+    s = scenes(idx)
+    p = z.RenderParams(w, h, 24, depth, sample_chunk=7)
+    gpu, gs, rows = z.render_progress(s, s.camera, p)
+    ref, rs, rrows = O.render_scanlines(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+    np.testing.assert_array_equal(rows, rrows)
+
+
 def test_c5_substitute_bit_exact(scenes):
     """Scene 6, the stated C5 substitute: 1.6 M subdivided teapot triangles
     (reference BVH 1 894 803 nodes, depth 39) with image-textured lambertians on both surfaces, so the
