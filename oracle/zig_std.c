@@ -306,7 +306,7 @@ float zs_pow(float x, float y) {
       ae += xe;
     }
     x1 *= x1;
-    xe <<= 1;
+    xe *= 2; /* xe << 1 without the UB of shifting a negative value */
     if (x1 < 0.5f) {
       x1 += x1;
       xe -= 1;

@@ -220,11 +220,11 @@ __device__ __forceinline__ float pow5_z(float x) {
   a1 *= x1;
   ae += xe;
   x1 *= x1;
-  xe <<= 1;
+  xe *= 2;
   if (x1 < 0.5f) { x1 += x1; xe -= 1; }
   // i = 2
   x1 *= x1;
-  xe <<= 1;
+  xe *= 2;
   if (x1 < 0.5f) { x1 += x1; xe -= 1; }
   // i = 1
   a1 *= x1;

@@ -532,10 +532,10 @@ int zrt_scene_load(uint32_t scene_index, const char* assets_dir, zrt_scene_data*
   if (!out) return zrt::fail(ZRT_E_INVALID, "null out");
   *out = nullptr;
   try {
-    auto h = new zrt_scene_data;
+    auto h = std::make_unique<zrt_scene_data>();  // freed if buildScene throws
     h->sd = zrt::buildScene(scene_index, assets_dir ? assets_dir : "");
     if (camera) *camera = h->sd->camera.abi();
-    *out = h;
+    *out = h.release();
     return ZRT_OK;
   } catch (const zrt::Error& e) {
     return zrt::fail(e.code, e.what());
