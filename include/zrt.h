@@ -453,11 +453,17 @@ int zrt_bvh_build_device(const zrt_scene* scene, uint32_t device, zrt_bvh_node**
  * Evaluate the kernel's own device functions on inputs, for bit-exact
  * comparison with the oracle's restatements:
  *   fn 0 sin, 1 cos (std.math, Go/Cephes), 2 acos, 3 atan (musl), 4 sqrt,
- *   5 atan2(x[i], y[i]), 6 pow(x[i], 5.0), 7 x[i] / y[i].
+ *   5 atan2(x[i], y[i]), 6 pow(x[i], 5.0), 7 x[i] / y[i] (HIP's IEEE `/`),
+ *   8 1 / x[i] and 9 x[i] / y[i] through the kernel's short correctly rounded
+ *   sequences (rcp_rn / div_rn, device_math.hpp).
  * zrt_debug_rng writes n outputs of DefaultPrng.init(key).next() computed on
- * the device.  Both run on `device` and synchronise. */
+ * the device.  zrt_debug_division runs the device self-check of those short
+ * sequences against IEEE `/` (counts[5]: mismatches of the reciprocal over all
+ * 2^32 inputs, of division, unit(), 1/d and the jitter quotient over n hashed
+ * inputs each; all zero on a correct build).  All run on `device` and synchronise. */
 int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t n, uint32_t device);
 int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device);
+int zrt_debug_division(uint64_t n, uint64_t* counts, uint32_t device);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,36 @@ def test_device_math_bit_exact():
     assert same_bits(z.debug_math(7, a[:n], den), (a[:n] / den).astype(np.float32)).all(), "div"
 
 
+def _edge_floats():
+    f = np.float32
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 2 ** -126, -(2 ** -126), 2 ** -149,
+                         np.finfo(f).max, -np.finfo(f).max, 2.0 ** 126, 2.0 ** 125 * 1.9999999, 2 ** -50,
+                         2 ** 50, 2 ** -51, 2 ** 51, 1e-6, 1.52], f)
+    bits = np.random.default_rng(11).integers(0, 2 ** 32, 1 << 16, dtype=np.uint64).astype(np.uint32)
+    return np.concatenate([specials, bits.view(f)])
+
+
+def test_short_divisions_equal_ieee_on_edges():
+    """The kernel's short reciprocal / division sequences (device_math.hpp rcp_rn,
+    div_rn: v_rcp + Newton step, Markstein's correction, range-guarded) give HIP's
+    IEEE quotients bit for bit, on special values and random bit patterns."""
+    x = _edge_floats()
+    with np.errstate(all="ignore"):
+        assert same_bits(z.debug_math(8, x), (np.float32(1) / x).astype(np.float32)).all(), "rcp_rn"
+        y = np.roll(x, 7)
+        assert same_bits(z.debug_math(9, x, y), (x / y).astype(np.float32)).all(), "div_rn"
+        assert same_bits(z.debug_math(9, x, y), z.debug_math(7, x, y)).all(), "div_rn vs device IEEE"
+
+
+def test_short_divisions_device_self_check():
+    """zrt_debug_division: the reciprocal over all 2^32 inputs, and division, unit(),
+    1/d and the jitter quotient over 2^28 hashed inputs each (signed zeros,
+    subnormals, inf, NaN, every exponent, near-midpoint quotients), against the
+    device's own IEEE `/`: no mismatch."""
+    counts = z.debug_division(1 << 28)
+    assert counts == {"rcp_all_2p32": 0, "div": 0, "unit": 0, "inv_dir": 0, "jitter": 0}, counts
+
+
 # ---- whole-frame parity ---------------------------------------------------------
 
 CASES = [

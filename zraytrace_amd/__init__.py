@@ -335,6 +335,14 @@ def nodes_to_numpy(nodes, n):
     return a["min"].copy(), a["max"].copy(), a["left"].copy(), a["right"].copy()
 
 
+def debug_division(n: int = 1 << 30, device: int = 0) -> dict:
+    """Device self-check of the kernel's short correctly rounded divisions
+    (zrt_debug_division): mismatch counts against HIP's IEEE `/`."""
+    out = (C.c_uint64 * 5)()
+    check(lib().zrt_debug_division(n, out, device))
+    return dict(zip(("rcp_all_2p32", "div", "unit", "inv_dir", "jitter"), (int(v) for v in out)))
+
+
 def debug_math(fn: int, x, y=None, device: int = 0):
     x = np.ascontiguousarray(x, dtype=np.float32)
     out = np.empty_like(x)

@@ -83,7 +83,10 @@ struct KArgs {
   unsigned long long* __restrict__ scanlines;
   uint32_t* __restrict__ error_flag;
   float org[3], llc[3], hor[3], ver[3];
-  float f_width, f_height, color_scale, pad0;
+  // jitter (raytrace.zig:173-174) divides by width / height: (x + r - 0.5) lies
+  // in {+0} u [2^-23, 65536], so dev::div_core with inv_* = RN(1 / width) (IEEE on
+  // the host) is the IEEE quotient with no range check
+  float f_width, f_height, color_scale, inv_width, inv_height;
   uint32_t width, height, xbound, spp, max_depth;
   uint32_t tiles_x, rank, world, total_work;
   uint32_t n_list, stack_depth, n_lanes;
@@ -257,7 +260,36 @@ __device__ __forceinline__ V3 scale(V3 a, float s) { return mk(a.x * s, a.y * s,
 __device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ V3 unit(V3 v) {  // vector.zig:88-92
   const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
+  // v.k / l as dev::div_core over one reciprocal of l (12 VALU instead of 30):
+  // bit-identical to the three IEEE divisions while l and every quotient lie in
+  // [2^-50, 2^50] (|quotient| <= 1 here); a zero / tiny component or a degenerate
+  // l takes the IEEE divisions (zero's sign, NaN of 0/0, inf)
+  const float y = dev::rcp_core(l);
+  const float qx = v.x * y, qy = v.y * y, qz = v.z * y;
+  const float qmin = __builtin_fminf(__builtin_fminf(__builtin_fabsf(qx), __builtin_fabsf(qy)), __builtin_fabsf(qz));
+  if (__builtin_expect(ZRT_FAST_DIV && l >= 0x1p-50f && l <= 0x1p50f && qmin >= 0x1p-50f, 1))
+    return mk(__builtin_fmaf(__builtin_fmaf(-qx, l, v.x), y, qx), __builtin_fmaf(__builtin_fmaf(-qy, l, v.y), y, qy),
+              __builtin_fmaf(__builtin_fmaf(-qz, l, v.z), y, qz));
   return mk(v.x / l, v.y / l, v.z / l);
+}
+// 1/d of aabb.zig:112 (one IEEE division per axis), bit for bit: dev::rcp_core
+// while every |d.k| lies in [2^-126, 2^126), else the IEEE divisions
+__device__ __forceinline__ void inv_dir(float dx, float dy, float dz, float& ix, float& iy, float& iz) {
+  const float lo = __builtin_fminf(__builtin_fminf(__builtin_fabsf(dx), __builtin_fabsf(dy)), __builtin_fabsf(dz));
+  const float hi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(dx), __builtin_fabsf(dy)), __builtin_fabsf(dz));
+  if (__builtin_expect(ZRT_FAST_DIV && lo >= 0x1p-126f && hi < 0x1p126f, 1)) {
+    ix = dev::rcp_core(dx);
+    iy = dev::rcp_core(dy);
+    iz = dev::rcp_core(dz);
+  } else {
+    ix = 1.0f / dx;
+    iy = 1.0f / dy;
+    iz = 1.0f / dz;
+  }
+}
+// 1/det of triangle.zig:63 for det >= 1e-6 (the only dets the hit test uses)
+__device__ __forceinline__ float inv_det_rn(float det) {
+  return __builtin_expect(ZRT_FAST_DIV && det < 0x1p126f, 1) ? dev::rcp_core(det) : 1.0f / det;
 }
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
 __device__ __forceinline__ V3 refract(V3 v, V3 n, float ratio) {  // vector.zig:132-137
@@ -365,7 +397,7 @@ __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, con
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float det = -dot(d, n);
   if (!(det >= 1e-6f)) return;
-  const float inv_det = 1.0f / det;
+  const float inv_det = inv_det_rn(det);
   const V3 ao = mk(r.ox - p0.x, r.oy - p0.y, r.oz - p0.z);
   const V3 dao = cross(ao, d);
   const V3 e1 = mk(p0.w, p1.x, p1.y);
@@ -1158,6 +1190,8 @@ __device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ 
 // ---------------------------------------------------------------------------
 constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
+constexpr float kInvPi = 1.0f / kPi;              // RN(1/pi), RN(1/(2pi)): dev::div_core's y
+constexpr float kInvTwoPi = 1.0f / kTwoPi;
 
 #ifndef ZRT_WAVES_PER_SIMD
 #define ZRT_WAVES_PER_SIMD 8  // binary/reference; A/B (tools/ab.sh): w5 11.2, w6 12.1, w7 12.4, w8 12.6 Gray/s
@@ -1218,7 +1252,7 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
         const float4 p2 = a.prims[3 * best + 2];
         const V3 n = mk(p2.y, p2.z, p2.w);
         const float det = -dot(d, n);
-        const float inv_det = 1.0f / det;
+        const float inv_det = inv_det_rn(det);
         const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
         const V3 dao = cross(ao, d);
         tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
@@ -1230,8 +1264,10 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
       if (need_uv) {  // sphere.zig:47-51
         const float theta = dev::acos_z(-outward.y);
         const float phi = dev::atan2_z(-outward.z, -outward.x) + kPi;
-        tu = phi / kTwoPi;
-        tv = theta / kPi;
+        // phi in {+0} u [2^-23, 2pi], theta in {+0} u [2^-12, pi]: dev::div_core's
+        // range, and +0 stays +0 (q = +0, r = +0, q + r*y = +0)
+        tu = dev::div_known(phi, kTwoPi, kInvTwoPi);
+        tv = dev::div_known(theta, kPi, kInvPi);
       }
     }
     bool front = true;
@@ -1258,13 +1294,13 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
       if (dot(nd, normal) > 0.0f) att = albedo(mat, a, tu, tv);
       else absorbed = true;
     } else {
-      const float ratio = front ? (1.0f / mat.ior()) : mat.ior();
+      const float ratio = front ? dev::rcp_rn(mat.ior()) : mat.ior();
       const V3 ud = unit(d);
       const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
       const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
       bool refl = ratio * sin_theta > 1.0f;
       if (!refl) {
-        const float r0 = (1.0f - ratio) / (1.0f + ratio);
+        const float r0 = dev::div_rn(1.0f - ratio, 1.0f + ratio);
         const float reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
         refl = reflectance > rand_float(rng);
       }
@@ -1392,8 +1428,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
       const uint64_t offset = (uint64_t)py * a.width + px;
       rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
-      const float u = ((float)px + rand_float(rng) - 0.5f) / a.f_width;
-      const float v = ((float)py + rand_float(rng) - 0.5f) / a.f_height;
+      const float u = dev::div_known((float)px + rand_float(rng) - 0.5f, a.f_width, a.inv_width);
+      const float v = dev::div_known((float)py + rand_float(rng) - 0.5f, a.f_height, a.inv_height);
       const V3 llc = mk(a.llc[0], a.llc[1], a.llc[2]);
       const V3 hor = mk(a.hor[0], a.hor[1], a.hor[2]);
       const V3 ver = mk(a.ver[0], a.ver[1], a.ver[2]);
@@ -1415,7 +1451,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       RayT r;
       r.ox = o.x; r.oy = o.y; r.oz = o.z;
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
-      r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+      inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
       float best_t = __builtin_inff();
       int best = -1;
       if (MODE == 0) {
@@ -1673,8 +1709,8 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
       const uint64_t offset = (uint64_t)py * a.width + px;
       rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
-      const float u = ((float)px + rand_float(rng) - 0.5f) / a.f_width;
-      const float vv = ((float)py + rand_float(rng) - 0.5f) / a.f_height;
+      const float u = dev::div_known((float)px + rand_float(rng) - 0.5f, a.f_width, a.inv_width);
+      const float vv = dev::div_known((float)py + rand_float(rng) - 0.5f, a.f_height, a.inv_height);
       const V3 llc = mk(a.llc[0], a.llc[1], a.llc[2]);
       const V3 hor = mk(a.hor[0], a.hor[1], a.hor[2]);
       const V3 ver = mk(a.ver[0], a.ver[1], a.ver[2]);
@@ -1687,7 +1723,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     if (STATS) ++c_rays;
     r.ox = o.x; r.oy = o.y; r.oz = o.z;
     r.dx = d.x; r.dy = d.y; r.dz = d.z;
-    r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+    inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
     best_t = __builtin_inff();
     best = -1;
     sp = 0;
@@ -1757,7 +1793,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   RayT r;
   r.ox = q[0]; r.oy = q[1]; r.oz = q[2];
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
-  r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
+  inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t c_nodes = 0, c_leaves = 0, c_tri = 0, c_sph = 0;
@@ -1856,9 +1892,91 @@ __global__ void debug_math_kernel(int fn, const float* __restrict__ x, const flo
     case 4: r = dev::sqrt_rn(a); break;
     case 5: r = dev::atan2_z(a, b); break;
     case 6: r = dev::pow5_z(a); break;
+    case 8: r = dev::rcp_rn(a); break;
+    case 9: r = dev::div_rn(a, b); break;
     default: r = a / b; break;
   }
   out[i] = r;
+}
+
+// Self-check of the short correctly rounded divisions (device_math.hpp) against
+// HIP's IEEE `/` on this device: counts[0] rcp_rn over all 2^32 inputs; [1] div_rn
+// over n hashed pairs (every exponent, signed zeros, subnormals, inf, NaN, and
+// dividends near short multiples of the divisor); [2] unit() over n vectors (wide
+// exponents, zero / tiny components); [3] inv_dir over n triples; [4] the jitter
+// quotient (x + r - 0.5) / width with y = RN(1/width) over n (width, x, r) draws.
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return uint32_t(x);
+}
+__device__ __forceinline__ bool same_f(float x, float y) {
+  return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y);
+}
+__device__ __forceinline__ float wild_float(uint32_t h, uint32_t h2) {  // any class, biased to edges
+  switch (h2 & 15) {
+    case 0: return __uint_as_float(h & 0x807fffffu);                       // +-0, subnormal
+    case 1: return __uint_as_float((h & 0x807fffffu) | 0x7f800000u);        // +-inf, NaN
+    case 2: return __uint_as_float((h & 0x80ffffffu) | (((h2 >> 4) & 3u) << 23) | 0x3f000000u);  // near 1
+    default: return __uint_as_float(h);                                     // any pattern
+  }
+}
+__global__ void debug_division_kernel(uint64_t n, unsigned long long* __restrict__ counts) {
+  const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+  for (uint64_t i = tid; i < (1ull << 32); i += stride) {
+    const float b = __uint_as_float(uint32_t(i));
+    c0 += same_f(dev::rcp_rn(b), 1.0f / b) ? 0u : 1u;
+  }
+  for (uint64_t i = tid; i < n; i += stride) {
+    const uint32_t h0 = mix32(8 * i), h1 = mix32(8 * i + 1), h2 = mix32(8 * i + 2), h3 = mix32(8 * i + 3);
+    const uint32_t h4 = mix32(8 * i + 4), h5 = mix32(8 * i + 5);
+    // [1] div_rn
+    float a = wild_float(h0, h2), b = wild_float(h1, h2 >> 8);
+    if ((h3 & 3) == 0) {  // a close to a short multiple of b (quotients near rounding midpoints)
+      const float k = float(int(h3 >> 20) + 1) * 0.0009765625f;
+      a = __uint_as_float(__float_as_uint(b * k) + int((h3 >> 2) & 7) - 3);
+    }
+    c1 += same_f(dev::div_rn(a, b), a / b) ? 0u : 1u;
+    // [2] unit(): components of one vector share an exponent window, some zero / tiny
+    const int e0 = int(h4 & 255) - 128;
+    V3 v;
+    float* vp = &v.x;
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t hk = mix32(8 * i + 6 + uint64_t(k) * 0x100000000ull);
+      const int e = e0 + int((hk >> 24) & 31) - 16;
+      const uint32_t bexp = uint32_t(e + 127 < 1 ? 0 : e + 127 > 254 ? 254 : e + 127);
+      float x = __uint_as_float((hk & 0x807fffffu) | (bexp << 23));
+      if (((h5 >> (4 * k)) & 15) == 0) x = (hk & 1) ? -0.0f : 0.0f;
+      if (((h5 >> (4 * k)) & 15) == 1) x = __uint_as_float(hk & 0x800fffffu);  // subnormal
+      vp[k] = x;
+    }
+    const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
+    const V3 u = unit(v);
+    c2 += (same_f(u.x, v.x / l) && same_f(u.y, v.y / l) && same_f(u.z, v.z / l)) ? 0u : 1u;
+    // [3] inv_dir over the same triples and over unit directions
+    float ix, iy, iz;
+    inv_dir(v.x, v.y, v.z, ix, iy, iz);
+    c3 += (same_f(ix, 1.0f / v.x) && same_f(iy, 1.0f / v.y) && same_f(iz, 1.0f / v.z)) ? 0u : 1u;
+    inv_dir(u.x, u.y, u.z, ix, iy, iz);
+    c3 += (same_f(ix, 1.0f / u.x) && same_f(iy, 1.0f / u.y) && same_f(iz, 1.0f / u.z)) ? 0u : 1u;
+    // [4] jitter (raytrace.zig:173): width in [1, 65535], x < 65536, r = Random.float
+    const float w = float((h0 & 0xffffu) | 1u) + float((h1 >> 16) & 0xfffeu);
+    const float fw = w > 65535.0f ? 65535.0f : w;
+    const float px = float(h2 & 0xffffu) * ((h3 >> 30) ? 1.0f : 0.0f);  // many x = 0 (tiny quotients)
+    const float r = __uint_as_float((0x7fu << 23) | (h4 >> 9)) - 1.0f;
+    const float num = px + r - 0.5f;
+    c4 += same_f(dev::div_core(num, fw, 1.0f / fw), num / fw) ? 0u : 1u;
+  }
+  if (c0) atomicAdd(&counts[0], (unsigned long long)c0);
+  if (c1) atomicAdd(&counts[1], (unsigned long long)c1);
+  if (c2) atomicAdd(&counts[2], (unsigned long long)c2);
+  if (c3) atomicAdd(&counts[3], (unsigned long long)c3);
+  if (c4) atomicAdd(&counts[4], (unsigned long long)c4);
 }
 
 template <int PRNG>
@@ -2733,6 +2851,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     }
     a.f_width = float(p->width);
     a.f_height = float(p->height);
+    a.inv_width = 1.0f / a.f_width;  // IEEE RN(1/width): dev::div_core's y
+    a.inv_height = 1.0f / a.f_height;
     a.color_scale = 1.0f / float(p->samples_per_pixel);  // raytrace.zig:157
     a.width = p->width;
     a.height = p->height;
@@ -3355,6 +3475,24 @@ int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t 
     HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, dout.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_debug_division(uint64_t n, uint64_t* counts, uint32_t device) {
+  if (!counts) return fail(ZRT_E_INVALID, "null argument");
+  int rc = zrt::check_device(int(device));
+  if (rc) return rc;
+  try {
+    HIPCHK(hipSetDevice(int(device)));
+    zrt::DevBuf<unsigned long long> d;
+    d.alloc(5);
+    HIPCHK(hipMemset(d.p, 0, 5 * sizeof(unsigned long long)));
+    hipLaunchKernelGGL(zrt::debug_division_kernel, dim3(8192), dim3(256), 0, 0, n, d.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(counts, d.p, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
