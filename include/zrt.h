@@ -458,8 +458,8 @@ int zrt_bvh_build_device(const zrt_scene* scene, uint32_t device, zrt_bvh_node**
  *   sequences (rcp_rn / div_rn, device_math.hpp).
  * zrt_debug_rng writes n outputs of DefaultPrng.init(key).next() computed on
  * the device.  zrt_debug_division runs the device self-check of those short
- * sequences against IEEE `/` (counts[5]: mismatches of the reciprocal over all
- * 2^32 inputs, of division, unit(), 1/d and the jitter quotient over n hashed
+ * sequences against IEEE `/` and sqrtf (counts[5]: mismatches of the reciprocal
+ * and the square root over all 2^32 inputs, of division, unit(), 1/d and the jitter quotient over n hashed
  * inputs each; all zero on a correct build).  All run on `device` and synchronise. */
 int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t n, uint32_t device);
 int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device);

@@ -79,24 +79,26 @@ def _edge_floats():
 
 
 def test_short_divisions_equal_ieee_on_edges():
-    """The kernel's short reciprocal / division sequences (device_math.hpp rcp_rn,
-    div_rn: v_rcp + Newton step, Markstein's correction, range-guarded) give HIP's
-    IEEE quotients bit for bit, on special values and random bit patterns."""
+    """The kernel's short reciprocal / division / sqrt sequences (device_math.hpp
+    rcp_rn, div_rn, sqrt_rn: v_rcp + Newton step, Markstein's correction, v_sqrt + FMA
+    fix-up, range-guarded) give IEEE results bit for bit, on special values and
+    random bit patterns."""
     x = _edge_floats()
     with np.errstate(all="ignore"):
         assert same_bits(z.debug_math(8, x), (np.float32(1) / x).astype(np.float32)).all(), "rcp_rn"
         y = np.roll(x, 7)
         assert same_bits(z.debug_math(9, x, y), (x / y).astype(np.float32)).all(), "div_rn"
         assert same_bits(z.debug_math(9, x, y), z.debug_math(7, x, y)).all(), "div_rn vs device IEEE"
+        assert same_bits(z.debug_math(4, x), np.sqrt(x)).all(), "sqrt_rn"
 
 
 def test_short_divisions_device_self_check():
-    """zrt_debug_division: the reciprocal over all 2^32 inputs, and division, unit(),
+    """zrt_debug_division: the reciprocal and sqrt over all 2^32 inputs, and division, unit(),
     1/d and the jitter quotient over 2^28 hashed inputs each (signed zeros,
     subnormals, inf, NaN, every exponent, near-midpoint quotients), against the
     device's own IEEE `/`: no mismatch."""
     counts = z.debug_division(1 << 28)
-    assert counts == {"rcp_all_2p32": 0, "div": 0, "unit": 0, "inv_dir": 0, "jitter": 0}, counts
+    assert counts == {"rcp_sqrt_all_2p32": 0, "div": 0, "unit": 0, "inv_dir": 0, "jitter": 0}, counts
 
 
 # ---- whole-frame parity ---------------------------------------------------------

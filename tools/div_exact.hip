@@ -86,6 +86,37 @@ __global__ void div_rand(uint64_t n, int E, unsigned long long* bad, uint32_t* f
   }
 }
 
+// v_sqrt_f32 alone, and v_sqrt + LLVM's +-1 ulp fix-up without the range scaling,
+// against IEEE sqrtf over all 2^32 patterns: counts[e] per biased exponent
+__global__ void sqrt_all(unsigned long long* raw, unsigned long long* fix) {
+  const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = tid; i < (1ull << 32); i += stride) {
+    const float x = __uint_as_float(uint32_t(i));
+    const float ref = __builtin_sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    if (!same(ref, s)) atomicAdd(&raw[(uint32_t(i) >> 23) & 0xff], 1ull);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float f = s;
+    if (__builtin_fmaf(-sd, s, x) <= 0.0f) f = sd;
+    if (__builtin_fmaf(-su, s, x) > 0.0f) f = su;
+    if (!same(ref, f)) atomicAdd(&fix[(uint32_t(i) >> 23) & 0xff], 1ull);
+  }
+}
+
+static void print_counts(const char* name, const unsigned long long* h) {
+  unsigned long long tot = 0;
+  for (int e = 0; e < 256; ++e) tot += h[e];
+  std::printf(", \"%s\": {\"mismatches\": %llu, \"by_exponent\": {", name, tot);
+  bool c = false;
+  for (int e = 0; e < 256; ++e)
+    if (h[e]) {
+      std::printf("%s\"%d\": %llu", c ? ", " : "", e, h[e]);
+      c = true;
+    }
+  std::printf("}}");
+}
+
 int main(int argc, char** argv) {
   const uint64_t n_div = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : (1ull << 34);
   unsigned long long* counts;
@@ -126,6 +157,19 @@ int main(int argc, char** argv) {
                 (unsigned long long)n_div, h[0]);
     for (unsigned k = 0; k < hn && k < 32; ++k) std::printf("%s[\"0x%08x\", \"0x%08x\"]", k ? ", " : "", hf[2 * k], hf[2 * k + 1]);
     std::printf("]}");
+  }
+  {
+    unsigned long long *raw, *fix;
+    CHK(hipMalloc(&raw, 256 * sizeof(unsigned long long)));
+    CHK(hipMalloc(&fix, 256 * sizeof(unsigned long long)));
+    CHK(hipMemset(raw, 0, 256 * sizeof(unsigned long long)));
+    CHK(hipMemset(fix, 0, 256 * sizeof(unsigned long long)));
+    sqrt_all<<<8192, 256>>>(raw, fix);
+    CHK(hipDeviceSynchronize());
+    CHK(hipMemcpy(h, raw, sizeof h, hipMemcpyDeviceToHost));
+    print_counts("v_sqrt", h);
+    CHK(hipMemcpy(h, fix, sizeof h, hipMemcpyDeviceToHost));
+    print_counts("v_sqrt_fixup", h);
   }
   std::printf("}\n");
   return 0;

@@ -8,6 +8,6 @@ export TMPDIR=/tmp
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
-bash tools/ab.sh $T/c4 2 default slowdiv -- --steps 5 --warmup 2 --no-reference-check || exit 1
-bash tools/ab.sh $T/c3 2 default slowdiv -- --scene 3 --width 1024 --height 1024 --spp 256 --steps 5 --warmup 2 --no-reference-check || exit 1
-bash tools/ab.sh $T/c2 1 default slowdiv -- --scene 1 --width 1000 --height 1000 --spp 1000 --depth 30 --steps 3 --warmup 1 --no-reference-check || exit 1
+bash tools/ab.sh $T/c4 2 default divonly slowdiv -- --steps 5 --warmup 2 --no-reference-check || exit 1
+bash tools/ab.sh $T/c3 2 default divonly slowdiv -- --scene 3 --width 1024 --height 1024 --spp 256 --steps 5 --warmup 2 --no-reference-check || exit 1
+bash tools/ab.sh $T/c2 1 default divonly slowdiv -- --scene 1 --width 1000 --height 1000 --spp 1000 --depth 30 --steps 3 --warmup 1 --no-reference-check || exit 1

@@ -340,7 +340,7 @@ def debug_division(n: int = 1 << 30, device: int = 0) -> dict:
     (zrt_debug_division): mismatch counts against HIP's IEEE `/`."""
     out = (C.c_uint64 * 5)()
     check(lib().zrt_debug_division(n, out, device))
-    return dict(zip(("rcp_all_2p32", "div", "unit", "inv_dir", "jitter"), (int(v) for v in out)))
+    return dict(zip(("rcp_sqrt_all_2p32", "div", "unit", "inv_dir", "jitter"), (int(v) for v in out)))
 
 
 def debug_math(fn: int, x, y=None, device: int = 0):

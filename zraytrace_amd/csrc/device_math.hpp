@@ -20,7 +20,6 @@ namespace dev {
 __device__ __forceinline__ float fmin_z(float x, float y) { return x < y ? x : y; }  // math.min
 __device__ __forceinline__ float fmax_z(float x, float y) { return x > y ? x : y; }  // math.max
 
-__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 
 __device__ __forceinline__ bool is_nan(float x) { return x != x; }
 __device__ __forceinline__ bool is_inf(float x) { return __builtin_fabsf(x) == __builtin_inff(); }
@@ -50,6 +49,9 @@ __device__ __forceinline__ float div_core(float a, float b, float y) {
 #ifndef ZRT_FAST_DIV
 #define ZRT_FAST_DIV 1  // 0: every reciprocal / division through HIP's IEEE `/` (A/B builds)
 #endif
+#ifndef ZRT_FAST_SQRT
+#define ZRT_FAST_SQRT ZRT_FAST_DIV  // 0: HIP's IEEE sqrtf
+#endif
 __device__ __forceinline__ bool rcp_core_ok(float b) {
   const float m = __builtin_fabsf(b);
   return ZRT_FAST_DIV && m >= 0x1p-126f && m < 0x1p126f;  // false for NaN
@@ -63,6 +65,23 @@ __device__ __forceinline__ float rcp_rn(float b) {
   if (__builtin_expect(rcp_core_ok(b), 1)) return rcp_core(b);
   return 1.0f / b;
 }
+// sqrt_core: v_sqrt_f32 (1 ulp) and LLVM's +-1 ulp fix-up by FMA residuals, without
+//   the scaling of small inputs and the zero / inf class select HIP's IEEE sqrtf adds
+//   (9 VALU instead of 16).  Equal to IEEE sqrtf for every x >= 2^-104 (and +inf):
+//   all 2^32 inputs checked on an MI355X (tools/div_exact.hip, zrt_debug_division).
+__device__ __forceinline__ float sqrt_core(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+  const float su = __uint_as_float(__float_as_uint(s) + 1u);
+  const float f = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+  return __builtin_fmaf(-su, s, x) > 0.0f ? su : f;
+}
+// sqrt, bit for bit (IEEE for zero, subnormal, negative and NaN inputs)
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if (__builtin_expect(ZRT_FAST_SQRT && x >= 0x1p-100f, 1)) return sqrt_core(x);
+  return __builtin_sqrtf(x);
+}
+
 // a / b, bit for bit
 __device__ __forceinline__ float div_rn(float a, float b) {
   const float mb = __builtin_fabsf(b);

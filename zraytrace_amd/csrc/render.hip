@@ -1900,7 +1900,8 @@ __global__ void debug_math_kernel(int fn, const float* __restrict__ x, const flo
 }
 
 // Self-check of the short correctly rounded divisions (device_math.hpp) against
-// HIP's IEEE `/` on this device: counts[0] rcp_rn over all 2^32 inputs; [1] div_rn
+// HIP's IEEE `/` and sqrtf on this device: counts[0] rcp_rn and sqrt_rn over all
+// 2^32 inputs; [1] div_rn
 // over n hashed pairs (every exponent, signed zeros, subnormals, inf, NaN, and
 // dividends near short multiples of the divisor); [2] unit() over n vectors (wide
 // exponents, zero / tiny components); [3] inv_dir over n triples; [4] the jitter
@@ -1931,6 +1932,7 @@ __global__ void debug_division_kernel(uint64_t n, unsigned long long* __restrict
   for (uint64_t i = tid; i < (1ull << 32); i += stride) {
     const float b = __uint_as_float(uint32_t(i));
     c0 += same_f(dev::rcp_rn(b), 1.0f / b) ? 0u : 1u;
+    c0 += same_f(dev::sqrt_rn(b), __builtin_sqrtf(b)) ? 0u : 1u;
   }
   for (uint64_t i = tid; i < n; i += stride) {
     const uint32_t h0 = mix32(8 * i), h1 = mix32(8 * i + 1), h2 = mix32(8 * i + 2), h3 = mix32(8 * i + 3);
@@ -1955,7 +1957,7 @@ __global__ void debug_division_kernel(uint64_t n, unsigned long long* __restrict
       if (((h5 >> (4 * k)) & 15) == 1) x = __uint_as_float(hk & 0x800fffffu);  // subnormal
       vp[k] = x;
     }
-    const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
+    const float l = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
     const V3 u = unit(v);
     c2 += (same_f(u.x, v.x / l) && same_f(u.y, v.y / l) && same_f(u.z, v.z / l)) ? 0u : 1u;
     // [3] inv_dir over the same triples and over unit directions
