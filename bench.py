@@ -158,19 +158,25 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(scene, scene_index, depth):
+def cpu_baseline(scene, scene_index, depth, target_s=15.0):
     """The oracle (single-threaded C restatement, reference RNG stream) on a
-    bounded sample of the same scene at the bench's depth: 128x128 @ 4 spp, or
-    16x16 @ 1 spp for a mesh of > 100k primitives (the reference's loose slab
-    test makes its traversal cost grow with the tree).  Also config C1 in full
-    (scene 1, 256x256 @ 16 spp, depth 30: BASELINE.md §3)."""
+    bounded sample of the same scene at the bench's depth: 128x128 pixels (16x16
+    for a mesh of > 100k primitives, whose reference loose slab test visits most of
+    the tree per ray), one probe sample per pixel, then as many samples per pixel
+    as fill about `target_s` seconds of one core.  Also config C1 in full (scene
+    1, 256x256 @ 16 spp, depth 30: BASELINE.md section 3)."""
     import zraytrace_amd as z
     from oracle import oracle_py as O
     big = scene.view.contents.n_prims > 100_000
     w = h = 16 if big else 128
-    spp = 1 if big else 4
-    p = z.RenderParams(w, h, spp, depth, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
+    p = z.RenderParams(w, h, 1, depth, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
     _, st = O.render(scene.view, scene.camera, p)
+    probe_s = st["render_ms"] / 1e3
+    spp = 1
+    if probe_s < target_s / 2:
+        spp = max(1, min(4096, int(target_s / max(probe_s, 1e-4))))
+        p = z.RenderParams(w, h, spp, depth, rng_mode=z.ZRT_RNG_REFERENCE_STREAM)
+        _, st = O.render(scene.view, scene.camera, p)
     dt = st["render_ms"] / 1e3  # the sampling loop only; its BVH build is timed apart (raytrace.zig:150)
     s1 = z.load_scene(1)
     _, c1 = O.render(s1.view, s1.camera, z.RenderParams(256, 256, 16, 30, rng_mode=z.ZRT_RNG_REFERENCE_STREAM))

@@ -361,7 +361,7 @@ constexpr float kOpen = ZRT_OPEN_MARGIN;
 
 template <bool TIE, bool TRACK>
 __device__ __forceinline__ void accept_hit(float t, int slot, float& best_t, int& best, const RayT& r,
-                                           const float* leafp) {
+                                           float entry) {
   if (!TRACK) {
     const bool in_range = TIE ? (t < best_t || (t == best_t && slot < best)) : (t < best_t);
     if (in_range) {
@@ -373,13 +373,10 @@ __device__ __forceinline__ void accept_hit(float t, int slot, float& best_t, int
   const float bt = __builtin_fabsf(best_t);
   if (t < bt || (t == bt && slot < best)) {
     bool near = t < bt ? bt <= t * kNearTie : best_t < 0.0f;  // an equal-t swap keeps the flag
-    if (leafp) {
-      // FAST: the leaf's loose entry E (aabb.zig:109-127; its near planes come first
-      // in the octant copy) above the hit by more than the band also flags the ray
-      const float e = __builtin_fmaxf(__builtin_fmaxf((leafp[0] - r.ox) * r.ix, (leafp[4] - r.oy) * r.iy),
-                                      __builtin_fmaxf((leafp[8] - r.oz) * r.iz, 0.001f));
-      near = near || e > t * kNearTie;
-    }
+    // FAST: the leaf's loose entry E (aabb.zig:109-127, >= t_min > 0; the slot's
+    // `en` of wide_iter, bit for bit) above the hit by more than the band also
+    // flags the ray; entry < 0: no leaf entry to check (the other traversals)
+    near = near || entry > t * kNearTie;
     best_t = near ? -t : t;
     best = slot;
   } else if (t > bt && t <= bt * kNearTie) {
@@ -392,7 +389,7 @@ __device__ __forceinline__ void accept_hit(float t, int slot, float& best_t, int
 // equal-t ties going to the lower slot (= earlier in the reference's DFS).
 template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, const float4 p2, int slot,
-                                           const RayT& r, float& best_t, int& best, const float* leafp = nullptr) {
+                                           const RayT& r, float& best_t, int& best, float entry = -1.0f) {
   const V3 n = mk(p2.y, p2.z, p2.w);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float det = -dot(d, n);
@@ -405,20 +402,20 @@ __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, con
   const float u = dot(e2, dao) * inv_det;
   const float v = -dot(e1, dao) * inv_det;
   const float t = dot(ao, n) * inv_det;
-  if (t > 0.001f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, leafp);
+  if (t > 0.001f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, entry);
 }
 
 template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void tri_test(const float4* __restrict__ prims, int slot, const RayT& r,
-                                         float& best_t, int& best, const float* leafp = nullptr) {
+                                         float& best_t, int& best, float entry = -1.0f) {
   tri_test_v<TIE, TRACK>(prims[3 * slot + 0], prims[3 * slot + 1], prims[3 * slot + 2], slot, r, best_t, best,
-                         leafp);
+                         entry);
 }
 
 // Sphere.hit (sphere.zig:31-41, 53-56): nearest root in (t_min, t_max).
 template <bool TIE, bool TRACK = false>
 __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT& r, float& best_t,
-                                            int& best, const float* leafp = nullptr) {
+                                            int& best, float entry = -1.0f) {
   const V3 oc = mk(r.ox - c.x, r.oy - c.y, r.oz - c.z);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float half_b = dot(oc, d);
@@ -428,21 +425,21 @@ __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT
   const float root = dev::sqrt_rn(disc);
   const float t1 = -half_b - root;
   const float t = (t1 > 0.001f) ? t1 : (-half_b + root);
-  if (t > 0.001f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, leafp);
+  if (t > 0.001f) accept_hit<TIE, TRACK>(t, slot, best_t, best, r, entry);
 }
 
 template <bool TIE, bool STATS, bool TRACK = false>
 __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int ref, const RayT& r,
                                           float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph,
-                                          const float* leafp = nullptr) {
+                                          float entry = -1.0f) {
   const int code = -ref - 1;
   const int slot = code >> 1;
   if (code & 1) {
     if (STATS) ++c_tri;
-    tri_test<TIE, TRACK>(prims, slot, r, best_t, best, leafp);
+    tri_test<TIE, TRACK>(prims, slot, r, best_t, best, entry);
   } else {
     if (STATS) ++c_sph;
-    sphere_test<TIE, TRACK>(prims[3 * slot], slot, r, best_t, best, leafp);
+    sphere_test<TIE, TRACK>(prims[3 * slot], slot, r, best_t, best, entry);
   }
 }
 
@@ -460,7 +457,7 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 template <bool TIE, bool STATS, bool TRACK = false>
 __device__ __forceinline__ void prim_test_uniform(const float4* __restrict__ prims, int ref, const RayT& r,
                                                   float& best_t, int& best, uint32_t& c_tri, uint32_t& c_sph,
-                                                  const float* leafp = nullptr) {
+                                                  float entry = -1.0f) {
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef const __attribute__((address_space(4))) float4 cfloat4;
   cfloat4* cp = (cfloat4*)prims;
@@ -471,10 +468,10 @@ __device__ __forceinline__ void prim_test_uniform(const float4* __restrict__ pri
   const int slot = code >> 1;
   if (code & 1) {
     if (STATS) ++c_tri;
-    tri_test_v<TIE, TRACK>(cp[3 * slot + 0], cp[3 * slot + 1], cp[3 * slot + 2], slot, r, best_t, best, leafp);
+    tri_test_v<TIE, TRACK>(cp[3 * slot + 0], cp[3 * slot + 1], cp[3 * slot + 2], slot, r, best_t, best, entry);
   } else {
     if (STATS) ++c_sph;
-    sphere_test<TIE, TRACK>(cp[3 * slot], slot, r, best_t, best, leafp);
+    sphere_test<TIE, TRACK>(cp[3 * slot], slot, r, best_t, best, entry);
   }
 }
 
@@ -985,7 +982,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         open &= open - 1u;
         const int L = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
         const int pb = as_int(k == 0 ? rb.x : k == 1 ? rb.y : k == 2 ? rb.z : rb.w);
-        const float* lp = ZRT_HAZARD_ENTRY ? reinterpret_cast<const float*>(leaf_q) + k : nullptr;
+        const float lp = ZRT_HAZARD_ENTRY ? (k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en) : -1.0f;
         if (STATS) {
           const int f = __builtin_amdgcn_readfirstlane(L);
           coh.ptests += 1u;
@@ -1006,7 +1003,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
   if (L != 0) {                                                                                     \
     const int pb = as_int(RB);                                                                      \
-    const float* lp = ZRT_HAZARD_ENTRY ? reinterpret_cast<const float*>(leaf_q) + K : nullptr;       \
+    const float lp = ZRT_HAZARD_ENTRY ? s##K.en : -1.0f;                                              \
     prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);              \
     if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp); \
   }
@@ -1041,6 +1038,17 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #endif
     } else {
       wide_load(g, sx, sy, sz, w);
+#if ZRT_AB_DOUBLE_NODE  // A/B probe only (never shipped): the same node read again from another octant copy
+      {
+        WideNode w2;
+        const uint32_t o2 = (v.base + a.wide_stride * (ZRT_AB_DOUBLE_NODE)) % (a.wide_stride * 8u);
+        wide_load(a.wnodes + o2 + 8u * (uint32_t)next, sx, sy, sz, w2);
+        const uint32_t x = __float_as_uint(w2.nx.x) ^ __float_as_uint(w2.ny.y) ^ __float_as_uint(w2.nz.z) ^
+                           __float_as_uint(w2.fx.w) ^ __float_as_uint(w2.fy.x) ^ __float_as_uint(w2.fz.y) ^
+                           __float_as_uint(w2.ra.z);
+        if (x == 0x7fc01234u) w.ra.x = w.ra.y;  // never true for the scenes measured
+      }
+#endif
     }
   }
   return true;
@@ -1134,9 +1142,18 @@ __device__ __forceinline__ V3 albedo(const MatReg& mr, const KArgs& a, float u, 
 }
 
 // raytrace.zig:53-58
-__device__ __forceinline__ V3 background(V3 d) {
-  const V3 u = unit(d);
-  const float t = 0.5f * (u.y + 1.0f);
+// unit(d).y alone (vector.zig:88-92 for the one component backgroundColor reads)
+__device__ __forceinline__ float unit_y(V3 v) {
+  const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
+  const float y = dev::rcp_core(l);
+  const float q = v.y * y;
+  if (__builtin_expect(ZRT_FAST_DIV && l >= 0x1p-50f && l <= 0x1p50f && __builtin_fabsf(q) >= 0x1p-50f, 1))
+    return __builtin_fmaf(__builtin_fmaf(-q, l, v.y), y, q);
+  return v.y / l;
+}
+
+__device__ __forceinline__ V3 background(V3 d) {  // raytrace.zig:53-58
+  const float t = 0.5f * (unit_y(d) + 1.0f);
   const float w = 1.0f - t;
   return mk(w + 0.5f * t, w + 0.7f * t, w + 1.0f * t);
 }
@@ -1959,7 +1976,7 @@ __global__ void debug_division_kernel(uint64_t n, unsigned long long* __restrict
     }
     const float l = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
     const V3 u = unit(v);
-    c2 += (same_f(u.x, v.x / l) && same_f(u.y, v.y / l) && same_f(u.z, v.z / l)) ? 0u : 1u;
+    c2 += (same_f(u.x, v.x / l) && same_f(u.y, v.y / l) && same_f(u.z, v.z / l) && same_f(unit_y(v), v.y / l)) ? 0u : 1u;
     // [3] inv_dir over the same triples and over unit directions
     float ix, iy, iz;
     inv_dir(v.x, v.y, v.z, ix, iy, iz);
