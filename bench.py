@@ -300,6 +300,17 @@ def main():
         pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
         roof = roofline(pmc_entry(pmc_key) if world == 1 else None, avg_kernel_s, algo, diag)
+        # what the render launch writes to memory: each work unit's
+        # 64 chunk sums (float4), and the attenuation rows past the LDS ones
+        # (float4; STATS counter kAttWrites of the diagnostic launch)
+        dc = fr.ctx.debug_counters(32)
+        wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 16 * int(dc[28])}
+        wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"]
+        pe = pmc_entry(pmc_key) if world == 1 else None
+        if pe and pe.get("write_size_kb"):
+            wb["pmc_write_B"] = int(pe["write_size_kb"] * 1024)
+            wb["predicted_over_pmc"] = round(wb["predicted_B"] / wb["pmc_write_B"], 3)
+        roof["write_budget"] = wb
         roof["kernel"] = f"render_kernel (BVH {args.traversal} traversal)"
         roof["counters_from"] = f"one untimed ZRT_FLAG_STATS launch (kernel {diag_kernel_ms:.1f} ms)"
         out = {

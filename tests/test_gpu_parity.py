@@ -518,6 +518,34 @@ def prim_array(v):
     return np.frombuffer(buf, dtype=dt)
 
 
+def test_trace_huge_triangle_det_bit_exact():
+    """A triangle with |e1 x e2| ~ 2.6e38: rays through it have det >= 2^126, where
+    1/det (triangle.zig:63) is subnormal and the short reciprocal is not exact, so
+    the scene takes the IEEE division (KArgs::tri_rcp_fast = 0).  Every traversal
+    and the list return the oracle's hits, as on the ordinary triangles beside it."""
+    import hazard_rays as H
+    big = 8.0e18
+    tris = [((-big, 0.0, -big), (-big, 0.0, big), (big, 0.0, -big))]  # e1 x e2 points up (+y)
+    rng = np.random.default_rng(5)
+    for _ in range(16):  # ordinary triangles just above it, hit from above
+        x, zc = rng.uniform(-1, 1, 2)
+        y, s = rng.uniform(0.05, 0.25), rng.uniform(0.1, 0.5)
+        tris.append(((x, y, zc), (x, y, zc + s), (x + s, y, zc)))
+    scene = H.scene_of([], tris)
+    n = 4000
+    # origins low enough that (o - a) . n stays finite (|n| = 2.56e38)
+    o = np.stack([rng.uniform(-1, 1, n), rng.uniform(0.3, 1.2, n), rng.uniform(-1, 1, n)], 1).astype(np.float32)
+    d = np.stack([rng.normal(0, 0.3, n), -np.ones(n), rng.normal(0, 0.3, n)], 1).astype(np.float32)
+    t_ref, p_ref = O.trace(scene, True, o, d)
+    assert (p_ref == 0).sum() > 1000, "rays must reach the huge triangle"
+    for trav in TRAVERSALS:
+        t, p = z.trace(scene, z.RenderParams(1, 1, 1, 1, traversal=trav), o, d)
+        assert_same_hits(t, p, t_ref, p_ref)
+    t_list, p_list = O.trace(scene, False, o, d)
+    t, p = z.trace(scene, z.RenderParams(1, 1, 1, 1, bounded_volume_hierarchy=False), o, d)
+    assert_same_hits(t, p, t_list, p_list)
+
+
 def test_trace_order_hazard_band_bit_exact():
     """rays whose smallest hit is a sphere hit t* lying
     below its own leaf's loose entry E by a relative (2^-15, 2^-14], with a

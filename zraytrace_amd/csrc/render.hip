@@ -106,6 +106,7 @@ struct KArgs {
   uint32_t lds_mat_off;   // the material table (n_mats DevMaterial), when mats_in_lds
   uint32_t n_mats, mats_in_lds;
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
+  uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -258,18 +259,28 @@ __device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, 
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ V3 scale(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+#ifndef ZRT_FD_UNIT  // per-site switches of the short divisions (A/B and register-pressure probes)
+#define ZRT_FD_UNIT ZRT_FAST_DIV
+#endif
+#ifndef ZRT_FD_INV
+#define ZRT_FD_INV ZRT_FAST_DIV
+#endif
+#ifndef ZRT_FD_TRI
+#define ZRT_FD_TRI ZRT_FAST_DIV
+#endif
 __device__ __forceinline__ V3 unit(V3 v) {  // vector.zig:88-92
   const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
   // v.k / l as dev::div_core over one reciprocal of l (12 VALU instead of 30):
-  // bit-identical to the three IEEE divisions while l and every quotient lie in
-  // [2^-50, 2^50] (|quotient| <= 1 here); a zero / tiny component or a degenerate
-  // l takes the IEEE divisions (zero's sign, NaN of 0/0, inf)
-  const float y = dev::rcp_core(l);
-  const float qx = v.x * y, qy = v.y * y, qz = v.z * y;
-  const float qmin = __builtin_fminf(__builtin_fminf(__builtin_fabsf(qx), __builtin_fabsf(qy)), __builtin_fabsf(qz));
-  if (__builtin_expect(ZRT_FAST_DIV && l >= 0x1p-50f && l <= 0x1p50f && qmin >= 0x1p-50f, 1))
-    return mk(__builtin_fmaf(__builtin_fmaf(-qx, l, v.x), y, qx), __builtin_fmaf(__builtin_fmaf(-qy, l, v.y), y, qy),
-              __builtin_fmaf(__builtin_fmaf(-qz, l, v.z), y, qz));
+  // bit-identical to the three IEEE divisions while l lies in [2^-50, 2^50] and
+  // every quotient in [2^-51, 1]; a zero / tiny component or a degenerate l takes
+  // the IEEE divisions (zero's sign, NaN of 0/0, inf)
+  // (the range is checked on the operands, |v.k| >= l * 2^-50, before any quotient
+  // exists, so each component's three steps need two registers at a time)
+  const float vmin = __builtin_fminf(__builtin_fminf(__builtin_fabsf(v.x), __builtin_fabsf(v.y)), __builtin_fabsf(v.z));
+  if (__builtin_expect(ZRT_FD_UNIT && l >= 0x1p-50f && l <= 0x1p50f && vmin >= l * 0x1p-50f, 1)) {
+    const float y = dev::rcp_core(l);
+    return mk(dev::div_core(v.x, l, y), dev::div_core(v.y, l, y), dev::div_core(v.z, l, y));
+  }
   return mk(v.x / l, v.y / l, v.z / l);
 }
 // 1/d of aabb.zig:112 (one IEEE division per axis), bit for bit: dev::rcp_core
@@ -277,7 +288,7 @@ __device__ __forceinline__ V3 unit(V3 v) {  // vector.zig:88-92
 __device__ __forceinline__ void inv_dir(float dx, float dy, float dz, float& ix, float& iy, float& iz) {
   const float lo = __builtin_fminf(__builtin_fminf(__builtin_fabsf(dx), __builtin_fabsf(dy)), __builtin_fabsf(dz));
   const float hi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(dx), __builtin_fabsf(dy)), __builtin_fabsf(dz));
-  if (__builtin_expect(ZRT_FAST_DIV && lo >= 0x1p-126f && hi < 0x1p126f, 1)) {
+  if (__builtin_expect(ZRT_FD_INV && lo >= 0x1p-126f && hi < 0x1p126f, 1)) {
     ix = dev::rcp_core(dx);
     iy = dev::rcp_core(dy);
     iz = dev::rcp_core(dz);
@@ -287,9 +298,13 @@ __device__ __forceinline__ void inv_dir(float dx, float dy, float dz, float& ix,
     iz = 1.0f / dz;
   }
 }
-// 1/det of triangle.zig:63 for det >= 1e-6 (the only dets the hit test uses)
-__device__ __forceinline__ float inv_det_rn(float det) {
-  return __builtin_expect(ZRT_FAST_DIV && det < 0x1p126f, 1) ? dev::rcp_core(det) : 1.0f / det;
+// 1/det of triangle.zig:63 for det >= 1e-6 (the only dets the hit test uses).
+// `fast` (wave-uniform, RayT::rcp_det): the scene's triangles keep det below
+// 2^126, so dev::rcp_core needs no per-lane guard (a per-lane branch here, in the
+// leaf loop, cost the FAST kernel 4 spilled VGPRs)
+__device__ __forceinline__ float inv_det_rn(float det, uint32_t fast) {
+  if (ZRT_FD_TRI && fast) return dev::rcp_core(det);
+  return 1.0f / det;
 }
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
 __device__ __forceinline__ V3 refract(V3 v, V3 n, float ratio) {  // vector.zig:132-137
@@ -306,6 +321,10 @@ struct RayT {
   float ox, oy, oz;
   float ix, iy, iz;  // 1/d per axis (aabb.zig:112 computes it per test; same bits)
   float dx, dy, dz;
+  // 1 when every triangle of the scene has |n| < 2^125 (host check), so a det of
+  // triangle.zig:61 that passes det >= 1e-6 lies in dev::rcp_core's range; a
+  // wave-uniform value (from KArgs), so the choice below is a scalar branch
+  uint32_t rcp_det;
 };
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
@@ -394,7 +413,7 @@ __device__ __forceinline__ void tri_test_v(const float4 p0, const float4 p1, con
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float det = -dot(d, n);
   if (!(det >= 1e-6f)) return;
-  const float inv_det = inv_det_rn(det);
+  const float inv_det = inv_det_rn(det, r.rcp_det);
   const V3 ao = mk(r.ox - p0.x, r.oy - p0.y, r.oz - p0.z);
   const V3 dao = cross(ao, d);
   const V3 e1 = mk(p0.w, p1.x, p1.y);
@@ -1145,10 +1164,8 @@ __device__ __forceinline__ V3 albedo(const MatReg& mr, const KArgs& a, float u, 
 // unit(d).y alone (vector.zig:88-92 for the one component backgroundColor reads)
 __device__ __forceinline__ float unit_y(V3 v) {
   const float l = dev::sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z);
-  const float y = dev::rcp_core(l);
-  const float q = v.y * y;
-  if (__builtin_expect(ZRT_FAST_DIV && l >= 0x1p-50f && l <= 0x1p50f && __builtin_fabsf(q) >= 0x1p-50f, 1))
-    return __builtin_fmaf(__builtin_fmaf(-q, l, v.y), y, q);
+  if (__builtin_expect(ZRT_FAST_DIV && l >= 0x1p-50f && l <= 0x1p50f && __builtin_fabsf(v.y) >= l * 0x1p-50f, 1))
+    return dev::div_core(v.y, l, dev::rcp_core(l));
   return v.y / l;
 }
 
@@ -1205,6 +1222,14 @@ __device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ 
 // ---------------------------------------------------------------------------
 // the sampling loop
 // ---------------------------------------------------------------------------
+// LDS-typed pointers are 32-bit: a generic (flat) float* into LDS costs a 64-bit
+// register pair across the whole loop (it was among the values the FAST kernel
+// spilled to scratch)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) float lds_float;
+#else
+typedef float lds_float;
+#endif
 constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
 constexpr float kInvPi = 1.0f / kPi;              // RN(1/pi), RN(1/(2pi)): dev::div_core's y
@@ -1227,7 +1252,7 @@ constexpr float kInvTwoPi = 1.0f / kTwoPi;
 // in the recursion's order when the path ends) and moves the ray on.
 template <bool STATS, class R>
 __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __restrict__ mats,
-                                           float* __restrict__ att_l, uint32_t gl, R& rng, int best, float best_t,
+                                           lds_float* __restrict__ att_l, uint32_t gl, R& rng, int best, float best_t,
                                            V3& o, V3& d, uint32_t& depth_left, bool& path_end, bool& sky, V3& L,
                                            uint32_t& c_bg, uint32_t& c_refl, uint32_t& c_shade, uint32_t& c_tex,
                                            Coh& coh) {
@@ -1269,7 +1294,7 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
         const float4 p2 = a.prims[3 * best + 2];
         const V3 n = mk(p2.y, p2.z, p2.w);
         const float det = -dot(d, n);
-        const float inv_det = inv_det_rn(det);
+        const float inv_det = inv_det_rn(det, a.tri_rcp_fast);
         const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
         const V3 dao = cross(ao, d);
         tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
@@ -1354,7 +1379,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
-  float* att_l = reinterpret_cast<float*>(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
   if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
@@ -1468,6 +1493,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       RayT r;
       r.ox = o.x; r.oy = o.y; r.oz = o.z;
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
+      r.rcp_det = a.tri_rcp_fast;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
       float best_t = __builtin_inff();
       int best = -1;
@@ -1599,7 +1625,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
-  float* att_l = reinterpret_cast<float*>(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
   if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
@@ -1622,6 +1648,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   rng.init(0);
   // the ray in flight and its suspended traversal
   RayT r{};
+  r.rcp_det = a.tri_rcp_fast;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -1810,6 +1837,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   RayT r;
   r.ox = q[0]; r.oy = q[1]; r.oz = q[2];
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
+  r.rcp_det = a.tri_rcp_fast;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
   float best_t = __builtin_inff();
   int best = -1;
@@ -2147,6 +2175,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint32_t> texels8;
   zrt::DevBuf<uint32_t> leaf_of_slot;
   uint32_t texel_bytes = 0;
+  uint32_t tri_rcp_fast = 1;
   zrt::DevBuf<float4> att;
   zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
@@ -2194,6 +2223,7 @@ struct HostScene {
   uint32_t n_prims = 0, n_nodes = 0, bvh_depth = 0;
   uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0, n_top = 0, n_mats = 0;
   uint32_t texel_bytes = 0;
+  uint32_t tri_rcp_fast = 1;  // KArgs::tri_rcp_fast
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
   std::vector<float> tex, lut;
@@ -2316,6 +2346,9 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       q[2] = make_float4(e2z, nx, ny, nz);
       tag |= 0x80000000u;
       sh = make_float4(nx / len, ny / len, nz / len, 0.0f);
+      // |det| = |d . n| <= |d| |n| < (1 + 2^-22) sqrt(3) 2^124 < 2^126 (NaN fails too)
+      const float mn = std::max(std::fabs(nx), std::max(std::fabs(ny), std::fabs(nz)));
+      if (!(mn < 0x1p124f)) c->tri_rcp_fast = 0;
     } else {
       q[0] = make_float4(p.center.x, p.center.y, p.center.z, p.radius);
       q[1] = make_float4(0, 0, 0, 0);
@@ -2430,6 +2463,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->wide_stack = h.wide_stack;
   c->wide_stride = h.wide_stride;
   c->texel_bytes = h.texel_bytes;
+  c->tri_rcp_fast = h.tri_rcp_fast;
   c->slot_to_prim = h.slot_to_prim;
 }
 
@@ -2883,6 +2917,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.world = p->world_size;
     a.total_work = work;
     a.n_list = c->use_bvh ? 0 : c->n_prims;
+    a.tri_rcp_fast = c->tri_rcp_fast;
     a.stack_depth = stack_depth;
     a.ref_stack = std::min(c->stack_depth, stack_depth);
     a.leaf_of_slot = c->leaf_of_slot.p;
@@ -3432,6 +3467,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.wide_stride = c->wide_stride;
     a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
     a.n_list = c->use_bvh ? 0 : c->n_prims;
+    a.tri_rcp_fast = c->tri_rcp_fast;
     a.stack_depth = stack_depth;
     a.ref_stack = c->stack_depth;
     a.leaf_of_slot = c->leaf_of_slot.p;
