@@ -301,11 +301,13 @@ def main():
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
         roof = roofline(pmc_entry(pmc_key) if world == 1 else None, avg_kernel_s, algo, diag)
         # what the render launch writes to memory: each work unit's
-        # 64 chunk sums (float4), and the attenuation rows past the LDS ones
-        # (float4; STATS counter kAttWrites of the diagnostic launch)
+        # 64 chunk sums (float4), the attenuation rows past the LDS ones (float4; STATS
+        # counter kAttWrites of the diagnostic launch) and, on deep trees, the traversal
+        # stack entries past the LDS rows (u32; kStackOvfWrites)
         dc = fr.ctx.debug_counters(32)
-        wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 16 * int(dc[28])}
-        wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"]
+        wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 16 * int(dc[28]),
+              "stack_rows_B": 4 * int(dc[30])}  # FAST stack entries past the LDS rows (kStackOvfWrites)
+        wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
         pe = pmc_entry(pmc_key) if world == 1 else None
         if pe and pe.get("write_size_kb"):
             wb["pmc_write_B"] = int(pe["write_size_kb"] * 1024)

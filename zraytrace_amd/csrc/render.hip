@@ -127,6 +127,9 @@ constexpr int kGlobalNodes = 24, kUniformNodes = 25, kPrimLaneTests = 26, kUnifo
 // STATS: attenuation-stack rows written to / read from global memory (rows past
 // the LDS ones): with the chunk sums, the loop's HBM writes
 constexpr int kAttWrites = 28, kAttReads = 29;
+// STATS: FAST traversal stack entries written to the global rows (deep trees:
+// rows past the LDS ones, 32-bit entries)
+constexpr int kStackOvfWrites = 30;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
 // cycle sums per loop section into counters[kProfSlot + section].
@@ -825,7 +828,7 @@ __device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict
 // farther ones pushed, branch-free.
 // STATS: coherence of the FAST loop's fetches (kGlobalNodes .. kUniformPrims)
 struct Coh {
-  uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0, attw = 0, attr = 0;
+  uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0, attw = 0, attr = 0, ovfw = 0;
   __device__ __forceinline__ void flush(unsigned long long* counters);
 };
 
@@ -974,8 +977,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
       const StackT e[3] = {e0, e1, e2};
 #pragma unroll
       for (uint32_t j = 0; j < 3; ++j) {
-        if (sp + j < rows) stk[(sp + j) * stride] = e[j];
-        else ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+        if (sp + j < rows) {
+          stk[(sp + j) * stride] = e[j];
+        } else {
+          ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+          if (STATS) ++coh.ovfw;
+        }
       }
     }
     const uint32_t nsp = sp + n - 1;
@@ -1199,6 +1206,7 @@ __device__ __forceinline__ void Coh::flush(unsigned long long* counters) {
   wave_add_u64(&counters[kUniformPrims], uprims);
   wave_add_u64(&counters[kAttWrites], attw);
   wave_add_u64(&counters[kAttReads], attr);
+  wave_add_u64(&counters[kStackOvfWrites], ovfw);
 }
 
 // ZRT_FLAG_SCANLINES: a finished unit's counters added to its frame rows.  The
