@@ -51,7 +51,7 @@ namespace zrt {
 //   a node index, child < 0 a primitive slot ref -(2*slot + kind) - 1.
 // prims: 3 x float4 per slot (slots in DFS leaf order, or list order):
 //   triangle {a.xyz, e1.x} {e1.yz, e2.xy} {e2.z, n.xyz}  (n = e1 x e2)
-//   sphere   {center.xyz, radius} {0} {0}
+//   sphere   {center.xyz, radius^2} {0} {0}   (radius * radius rounded once, on the host)
 // shade: 1 x float4 per slot: triangle {unit normal.xyz, tag},
 //   sphere {1/radius, 0, 0, tag}; tag = material | kind << 31 (as u32 bits)
 struct alignas(16) DevMaterial {
@@ -441,7 +441,7 @@ __device__ __forceinline__ void sphere_test(const float4 c, int slot, const RayT
   const V3 oc = mk(r.ox - c.x, r.oy - c.y, r.oz - c.z);
   const V3 d = mk(r.dx, r.dy, r.dz);
   const float half_b = dot(oc, d);
-  const float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - (c.w * c.w);
+  const float cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - c.w;  // c.w = RN(r * r)
   const float disc = half_b * half_b - cc;
   if (disc < 0.0f) return;
   const float root = dev::sqrt_rn(disc);
@@ -465,6 +465,9 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
   }
 }
 
+#ifndef ZRT_SORT_SKIP
+#define ZRT_SORT_SKIP 1  // FAST: skip the inner-child sort when no lane of the wave has two children to order
+#endif
 #ifndef ZRT_SCALAR_NODES
 #define ZRT_SCALAR_NODES 1  // FAST: a wide node every active lane reads next comes through the scalar cache
 #endif
@@ -957,6 +960,18 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
   float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
   const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
+#if ZRT_SORT_SKIP
+  if (__ballot(n > 1u) == 0ull) {
+    // every active lane follows at most one inner child: no sort, nothing to push
+    // (a wave-uniform branch around the 5 compare-exchanges and the 3 stores)
+    if (n != 0) {
+      next = k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3;
+    } else if (sp != 0) {
+      --sp;
+      next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+    }
+  } else {
+#endif
   // sort (entry, ref) ascending: 5 compare-exchanges
   cswap(k0, r0, k1, r1);
   cswap(k2, r2, k3, r3);
@@ -995,6 +1010,9 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     --sp;
     next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
   }
+#if ZRT_SORT_SKIP
+  }
+#endif
   // each lane walks ITS opened leaves in slot order, so lanes that opened
   // different slots share loop trips (the result is the closest t, ties to
   // the lower slot, order hazards flagged).  A/B against four unrolled slot
@@ -2358,7 +2376,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       const float mn = std::max(std::fabs(nx), std::max(std::fabs(ny), std::fabs(nz)));
       if (!(mn < 0x1p124f)) c->tri_rcp_fast = 0;
     } else {
-      q[0] = make_float4(p.center.x, p.center.y, p.center.z, p.radius);
+      q[0] = make_float4(p.center.x, p.center.y, p.center.z, p.radius * p.radius);  // sphere.zig:35 r*r, once
       q[1] = make_float4(0, 0, 0, 0);
       q[2] = make_float4(0, 0, 0, 0);
       sh = make_float4(1.0f / p.radius, 0.0f, 0.0f, 0.0f);  // sphere.zig:46 scale(1.0/radius)
