@@ -1823,6 +1823,9 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   }
 }
 
+#ifndef ZRT_ATT_ROWS_WF
+#define ZRT_ATT_ROWS_WF 4  // wavefront loop: attenuation rows kept in LDS (A/B: 2 = the lockstep kernel's)
+#endif
 #ifndef ZRT_WAVES_WF
 #define ZRT_WAVES_WF 4  // wavefront loop (MODE 4)
 #endif
@@ -2541,8 +2544,8 @@ struct LdsPlan {
   uint32_t stack_rows = 0, top_off = 0, att_off = 0, att_rows = 0, mat_off = 0, mats_in_lds = 0;
   size_t bytes = 0;
 };
-LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth) {
-  const uint32_t waves = mode == 3 ? ZRT_WAVES_WIDE : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
+LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf = false) {
+  const uint32_t waves = mode == 3 ? (wf ? ZRT_WAVES_WF : ZRT_WAVES_WIDE) : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
   // 256-thread blocks: `waves` blocks per CU; 1 KiB below the even share (a
   // block of exactly 32 KiB ran 8 % slower at 5 blocks per CU)
   const size_t budget = (160u << 10) / waves - (1u << 10);
@@ -2552,13 +2555,16 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1)
   // A/B (C4, interleaved): none 50.35, 1 row 50.57, 2 rows 50.70 Gray/s; 4 rows
   // (a 32 KiB block, the whole budget) 46.5
-  uint32_t want = 2;
+  // The wavefront loop runs 4 blocks per CU: its larger share holds 4 rows (its
+  // scenes, the textured C5 mesh, scatter more often)
+  const uint32_t att_cap = wf ? ZRT_ATT_ROWS_WF : 2u;
+  uint32_t want = att_cap;
   if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
   LdsPlan L;
   if (mode == 3 && !stk16) {
     // deep trees: the stack takes what the top nodes and two attenuation rows leave
-    want = std::min<uint32_t>(want, 2);
+    want = std::min<uint32_t>(want, att_cap);
     const size_t room = budget > top + want * row_att ? budget - top - want * row_att : 0;
     L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(stack_depth, uint32_t(room / (kBlock * entry))));
   } else {
@@ -2884,7 +2890,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth);
+    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
     int per_cu = 0;
