@@ -169,9 +169,6 @@ constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #ifndef ZRT_HAZARD_ENTRY
 #define ZRT_HAZARD_ENTRY 1  // also replay rays whose best hit lies below its own leaf's loose entry
 #endif
-#if ZRT_HAZARD_ENTRY && !ZRT_OCT_COPIES
-#error "the FAST entry test reads the near planes of the octant copies (ZRT_OCT_COPIES=1)"
-#endif
 #ifndef ZRT_LDS_TOP
 #define ZRT_LDS_TOP 1  // FAST: the wide tree's top levels read from LDS (0: A/B, every node from global memory)
 #endif
