@@ -577,3 +577,37 @@ def test_reference_box_excess_diagnostic(scenes):
     for k in ("box_excess_max_triangle", "box_excess_max_sphere"):
         assert np.isfinite(st[k]) and st[k] >= 0.0, (k, st[k])
     assert st["box_excess_max_triangle"] < 2 ** -12  # the bunny's triangles: far inside FAST's margin
+
+
+def _grazing_case(scenes, which):
+    """(scene view, origins, directions) of tests/grazing_rays.py for a mesh scene
+    or for bvh.zig:262-291's 3127 random spheres (which = "spheres")."""
+    import grazing_rays as G
+    if which == "spheres":
+        sph, _ = O.bvh_test_data(z.ZRT_PRNG_XOROSHIRO128, 42, 3127, 1)
+        view = sphere_scene(sph)
+        keep = view
+    else:
+        keep = scenes(which)
+        view = keep.view
+    pr = prim_array(view.contents if hasattr(view, "contents") else view)
+    mins, maxs, left, _, _ = O.bvh_build(view)
+    o, d = G.grazing_rays(pr, mins, maxs, left, n=6000, seed=7, span=float(np.max(maxs[0] - mins[0])))
+    return keep, view, o, d
+
+
+@pytest.mark.parametrize("which", [2, 3, 0, 4, "spheres"])
+def test_trace_grazing_rays_bit_exact(scenes, which):
+    """FAST culls a box only when the ray misses it by more
+    than the 2^-16 margin, on the assumption that such a box holds no primitive
+    the reference hits.  Rays in (or 1-4 ulps beside) the planes of box faces,
+    through the triangle vertices and sphere extremes those planes pass through,
+    and through leaf box corners and edges (tests/grazing_rays.py): every
+    traversal returns the oracle's surface and t bit for bit, the order effects
+    among them included (the reference BVH and the list disagree on 1-2 %)."""
+    keep, view, o, d = _grazing_case(scenes, which)
+    t_ref, p_ref = O.trace(view, True, o, d)
+    assert (p_ref >= 0).mean() > 0.5
+    for trav in TRAVERSALS:
+        t, p = z.trace(keep, z.RenderParams(1, 1, 1, 1, traversal=trav), o, d)
+        assert_same_hits(t, p, t_ref, p_ref)

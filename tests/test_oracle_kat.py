@@ -191,3 +191,21 @@ def test_oracle_scanlines_are_progress_deltas(scenes):
     for i, k in enumerate(("recursion_depth_hits", "reflections", "background_hits", "pixels_processed",
                            "samples_processed", "rays_processed")):
         assert tot[i] == st[k], k
+
+
+def test_grazing_rays_run_in_box_planes(scenes):
+    """tests/grazing_rays.py (used by the GPU parity test of FAST's narrowed box
+    test): most rays hit, over a third run exactly in an axis plane through a
+    box face (a zero direction component), and the construction reaches the
+    reference's order effects (BVH answer != list answer) on some of them."""
+    import grazing_rays as G
+    from test_gpu_parity import prim_array
+    s = scenes(2)
+    mins, maxs, left, _, _ = O.bvh_build(s.view)
+    o, d = G.grazing_rays(prim_array(s.view.contents), mins, maxs, left, n=3000, seed=7,
+                          span=float(np.max(maxs[0] - mins[0])))
+    t, p = O.trace(s.view, True, o, d)
+    _, pl = O.trace(s.view, False, o, d)
+    assert (p >= 0).mean() > 0.5
+    assert (d == 0).any(axis=1).mean() > 0.35
+    assert (p != pl).sum() > 10
