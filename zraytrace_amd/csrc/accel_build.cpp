@@ -28,6 +28,12 @@
 //                  ref a / ref b are its one or two primitive-slot refs of
 //                  render.hip (< 0; b == a for a one-primitive leaf);
 //     empty slot:  an empty box (min = +inf, max = -inf), never entered.
+//   An inner child's box is stored grown by `inflate` (render.hip passes 2^-19 x
+//   the scene's largest coordinate): a computed primitive hit lies outside its
+//   box by a few ulps of the coordinates, and growing the box in space grows
+//   each axis's t interval by that distance x |1/d_k| - the right slack for a
+//   ray (nearly) parallel to a box face, at no cost per node (DESIGN.md §3
+//   "Grazing rays").
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -157,7 +163,7 @@ void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
 
 }  // namespace
 
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels) {
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate) {
   WideBvh out;
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
@@ -279,6 +285,13 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels) 
         } else {
           ref = pos[size_t(wide_of[c])];
           ref_b = 0;
+          for (int a = 0; a < 3 && inflate > 0.0f; ++a) {  // grown outward, rounded outward
+            float lo = box.mn[a] - inflate, hi = box.mx[a] + inflate;
+            if (double(lo) > double(box.mn[a]) - double(inflate)) lo = std::nextafter(lo, -INFINITY);
+            if (double(hi) < double(box.mx[a]) + double(inflate)) hi = std::nextafter(hi, INFINITY);
+            box.mn[a] = lo;
+            box.mx[a] = hi;
+          }
         }
       }
       put4(q[0], k, box.mn[0]);

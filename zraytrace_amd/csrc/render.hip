@@ -107,6 +107,7 @@ struct KArgs {
   uint32_t n_mats, mats_in_lds;
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
+  float scene_extent;     // max |coordinate| of the primitives' boxes (RayT::slack)
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -325,7 +326,48 @@ struct RayT {
   // triangle.zig:61 that passes det >= 1e-6 lies in dev::rcp_core's range; a
   // wave-uniform value (from KArgs), so the choice below is a scalar branch
   uint32_t rcp_det;
+  // absolute slacks in t of the narrowed culls (ray_slack): entry > exit * (1 + 2^-16) + slack culls
+  float slack;      // reference boxes (leaf slots, BINARY, the replay)
+  float slack_far;  // inner wide slots (boxes stored grown): 0 unless |o| exceeds the scene extent
 };
+
+// A computed primitive hit lies outside its own box by a few ulps of the
+// coordinates involved (up to 4e-6 x max(scene extent, |o|) on the rays of
+// tests/grazing_rays.py, most of it along the ray).  In t that is the distance
+// times |1/d_k| on the axis it is measured along, unbounded for a ray (nearly)
+// parallel to a box face: the relative margin alone culled boxes the reference
+// opens and hits in (DESIGN.md §3 "Grazing rays").  With delta = 2^-19 x
+// max(scene extent, |o|):
+// * inner wide slots: their boxes are stored grown by 2^-19 x scene extent
+//   (accel_build.cpp), which grows each axis's t interval by exactly that
+//   distance x |1/d_k|, per axis, at no cost per node; slack_far adds what a ray
+//   from beyond the scene extent needs on top (0 for every render ray);
+// * reference boxes (leaf slots, the BINARY traversal, the replay), which must
+//   stay bit for bit: a uniform slack 2 x delta x max_k |1/d_k|.  A leaf slot
+//   that fails the narrowed test by less goes through the reference's own loose
+//   test (loose_slot), which decides it exactly; an axis-parallel ray (slack
+//   inf) gets the loose test on every leaf slot of the nodes it visits.
+// On the grazing rays no hit lies outside its box's t interval by more than 0.27
+// of delta x M + 2^-16 t (tools/grazing_excess.py).
+#ifndef ZRT_GRAZE_SLACK
+#define ZRT_GRAZE_SLACK 1  // 0: A/B only (round-2 margins, not exact on grazing rays)
+#endif
+#ifndef ZRT_GROW
+#define ZRT_GROW ZRT_GRAZE_SLACK  // A/B only: 0 stores inner boxes ungrown (not exact)
+#endif
+#ifndef ZRT_LEAF_SLACK
+#define ZRT_LEAF_SLACK ZRT_GRAZE_SLACK  // A/B only: 0 drops the leaf slots' slack (not exact)
+#endif
+__device__ __forceinline__ void ray_slack(float scene_extent, RayT& r) {
+  r.slack = r.slack_far = 0.0f;
+  if (!ZRT_GRAZE_SLACK) return;
+  const float om = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox), __builtin_fabsf(r.oy)),
+                                   __builtin_fabsf(r.oz));
+  const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ix), __builtin_fabsf(r.iy)),
+                                  __builtin_fabsf(r.iz));
+  r.slack = __builtin_fmaxf(__builtin_fmaxf(scene_extent, om), 0x1p-100f) * 0x1p-18f * m;
+  if (om > scene_extent) r.slack_far = (om - scene_extent) * 0x1p-18f * m;
+}
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
 // FAST additionally narrows the interval across axes (with a 2^-16 relative
@@ -351,7 +393,7 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && !(en > ex * 1.0000153f);
+    ok = ok && !(en > __builtin_fmaf(ex, 1.0000153f, r.slack));
     *entry = en;
   }
   return ok;
@@ -636,7 +678,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
-    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * kOpen, &e)) return;
+    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * kOpen + r.slack, &e)) return;
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
@@ -646,7 +688,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
         const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
         if (STATS) c_nodes += 2;
-        const float tb = __builtin_fabsf(best_t) * kOpen;
+        const float tb = __builtin_fabsf(best_t) * kOpen + r.slack;
         float el, er;
         const bool hl = box_test<true>(l0, l1, r, tb, &el);
         const bool hr = box_test<true>(r0, r1, r, tb, &er);
@@ -669,7 +711,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const int idx = stk[sp * stride];
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
-        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * kOpen, &e)) {
+        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * kOpen + r.slack, &e)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
           found = true;
@@ -733,7 +775,7 @@ __device__ __forceinline__ float wide_slot(float mnx, float mny, float mnz, floa
   const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, tb);
   const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
   const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-  bool ok = !(en > ex * 1.0000153f);
+  bool ok = !(en > __builtin_fmaf(ex, 1.0000153f, r.slack));
   if (leaf) ok = ok && (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) per axis
   return ok ? en : __builtin_inff();
 }
@@ -933,9 +975,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
   const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
   const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
-  // narrowed test: entry > exit * (1 + 2^-16) culls
-  const bool h0 = !(s0.en > s0.ex * 1.0000153f), h1 = !(s1.en > s1.ex * 1.0000153f);
-  const bool h2 = !(s2.en > s2.ex * 1.0000153f), h3 = !(s3.en > s3.ex * 1.0000153f);
+  // narrowed test: entry > exit * (1 + 2^-16) + slack culls (ray_slack: inner
+  // slots' boxes are stored grown, leaf slots' are the reference leaves')
+  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, 1.0000153f, r0 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
+  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, 1.0000153f, r1 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
+  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, 1.0000153f, r2 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
+  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, 1.0000153f, r3 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
@@ -945,10 +990,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
   const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
-    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
-    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
-    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
+    // (a hit may lie below its leaf's entry by the slack: loose test against tb + slack)
+    const float tl = tb + r.slack;
+    if (w0) o0 = loose_slot(q, 0, r, tl, sx, sy, sz);
+    if (w1) o1 = loose_slot(q, 1, r, tl, sx, sy, sz);
+    if (w2) o2 = loose_slot(q, 2, r, tl, sx, sy, sz);
+    if (w3) o3 = loose_slot(q, 3, r, tl, sx, sy, sz);
   }
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
   const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
@@ -1518,6 +1565,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
       r.rcp_det = a.tri_rcp_fast;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
+      ray_slack(a.scene_extent, r);
       float best_t = __builtin_inff();
       int best = -1;
       if (MODE == 0) {
@@ -1791,6 +1839,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     r.ox = o.x; r.oy = o.y; r.oz = o.z;
     r.dx = d.x; r.dy = d.y; r.dz = d.z;
     inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
+    ray_slack(a.scene_extent, r);
     best_t = __builtin_inff();
     best = -1;
     sp = 0;
@@ -1865,6 +1914,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
   r.rcp_det = a.tri_rcp_fast;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
+  ray_slack(a.scene_extent, r);
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t c_nodes = 0, c_leaves = 0, c_tri = 0, c_sph = 0;
@@ -2202,6 +2252,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint32_t> leaf_of_slot;
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
+  float scene_extent = 1.0f;
   zrt::DevBuf<float4> att;
   zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
@@ -2250,6 +2301,7 @@ struct HostScene {
   uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0, n_top = 0, n_mats = 0;
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;  // KArgs::tri_rcp_fast
+  float scene_extent = 0.0f;  // KArgs::scene_extent
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
   std::vector<float> tex, lut;
@@ -2324,7 +2376,11 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
     const double tw = now_ms();
-    const WideBvh wide = build_wide_bvh(leaves);
+    // the scene's largest coordinate (leaf boxes are unions of the primitives' boxes)
+    for (const RefLeaf& L : leaves)
+      for (int k = 0; k < 3; ++k)
+        c->scene_extent = std::max({c->scene_extent, std::fabs(L.mn[k]), std::fabs(L.mx[k])});
+    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? std::ldexp(c->scene_extent, -19) : 0.0f);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
@@ -2356,6 +2412,14 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   std::vector<float4> shade(slot_to_prim.size());
   for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
     const zrt_prim& p = s->prims[slot_to_prim[sl]];
+    if (p.kind == ZRT_PRIM_TRIANGLE) {
+      for (const auto& v : {p.a, p.b, p.c})
+        c->scene_extent = std::max({c->scene_extent, std::fabs(v.x), std::fabs(v.y), std::fabs(v.z)});
+    } else {
+      c->scene_extent = std::max({c->scene_extent, std::fabs(p.center.x) + std::fabs(p.radius),
+                                  std::fabs(p.center.y) + std::fabs(p.radius),
+                                  std::fabs(p.center.z) + std::fabs(p.radius)});
+    }
     float4* q = &prims[3 * sl];
     float4& sh = shade[sl];
     uint32_t tag = p.material;
@@ -2490,6 +2554,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->wide_stride = h.wide_stride;
   c->texel_bytes = h.texel_bytes;
   c->tri_rcp_fast = h.tri_rcp_fast;
+  c->scene_extent = h.scene_extent;
   c->slot_to_prim = h.slot_to_prim;
 }
 
@@ -2947,6 +3012,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.total_work = work;
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
+    a.scene_extent = c->scene_extent;
     a.stack_depth = stack_depth;
     a.ref_stack = std::min(c->stack_depth, stack_depth);
     a.leaf_of_slot = c->leaf_of_slot.p;
@@ -3497,6 +3563,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
+    a.scene_extent = c->scene_extent;
     a.stack_depth = stack_depth;
     a.ref_stack = c->stack_depth;
     a.leaf_of_slot = c->leaf_of_slot.p;
