@@ -4,12 +4,15 @@ grazing rays of tests/grazing_rays.py, against the FAST culls' margins (DESIGN.m
 each ray's hit; the hit point o + t*unit(d) is compared with the primitive's box
 (triangle: vertex min/max; sphere: center -+ r), axis by axis.
 
-A box FAST culls has entry > exit * (1 + 2^-16) + slack (render.hip ray_slack,
-slack = 2^-18 * max(scene extent, |o|) * max_k |1/d_k|); a hit outside its box by
-e_k on axis k lies e_k * |1/d_k| outside the box's t interval.  Printed: the largest
-spatial excess relative to max(scene extent, |o|), and the largest t-space excess as
-a fraction of half the cull margin (2^-19 ... * M + 2^-16 t) - below 1 means every
-hit of these rays would survive the cull.
+A box FAST culls has entry > exit * rel + slack (render.hip ray_slack: rel = 1 +
+2^-16 + 2^-18 M, slack = 2^-18 x the triangles' largest |coordinate| x M, M =
+max_k |1/d_k|); a hit outside its box by e_k on axis k lies e_k * |1/d_k| outside the
+box's t interval.  Printed: the largest spatial excess relative to max(scene extent,
+|o|), and the largest t-space excess as a fraction of half the cull margin, in the
+slack form (reference boxes; triangles and spheres apart: a sphere's hit point is
+on the ray, its excess is its error in t) and in the local form (2^-19 x the box's own largest
+|coordinate| x |1/d_k| + t (2^-16 + 2^-18 M) / 2: grown inner boxes, loose_slot) - below
+1 means every hit of these rays would survive the cull.
 
 usage: python tools/grazing_excess.py [scene ...]   (default 0 2 3 4)
 """
@@ -54,9 +57,21 @@ def main():
             inv = np.abs(1.0 / u)
         m = inv.max(1)
         et = np.nan_to_num(e * inv, nan=0.0, posinf=0.0).max(1)
-        half = 2.0 ** -19 * scale * m + t[h] * 2.0 ** -16
-        print(f"scene {w}: {int(h.sum())} hits, extent {extent:.4g}, spatial excess / scale max "
-              f"{(e.max(1) / scale).max():.3g}, t-space excess / half margin max {(et / half).max():.3g}")
+        ctri = max(np.abs(V[tri]).max(), 1e-30) if tri.any() else 1e-30
+        half = 2.0 ** -19 * ctri * m + t[h] * (2.0 ** -16 + 2.0 ** -18 * m) / 2
+        # the local form (inner wide boxes, loose_slot): per axis 2^-19 x the box's own
+        # largest |coordinate| (here the primitive's, the smallest box holding it)
+        # x |1/d_k|, plus t x (2^-16 + 2^-18 M) / 2
+        cp = np.maximum(np.abs(lo[p[h]]).max(1), np.abs(hi[p[h]]).max(1))
+        loc = np.nan_to_num(2.0 ** -19 * cp[:, None] * inv, nan=np.inf) + (t[h] * (2.0 ** -16 + 2.0 ** -18 * m) / 2)[:, None]
+        with np.errstate(invalid="ignore"):
+            rl = np.nan_to_num(e * inv / loc, nan=0.0).max(1)
+        th = tri[p[h]]
+        rs = et / half
+        print(f"scene {w}: {int(h.sum())} hits, extent {extent:.4g}, triangles' {ctri:.4g}; spatial excess / "
+              f"max(extent, |o|) max {(e.max(1) / scale).max():.3g}; t-space excess / half margin max: "
+              f"slack form triangles {rs[th].max() if th.any() else 0:.3g} spheres "
+              f"{rs[~th].max() if (~th).any() else 0:.3g}, local form {rl.max():.3g}")
 
 
 if __name__ == "__main__":

@@ -28,9 +28,9 @@
 //                  ref a / ref b are its one or two primitive-slot refs of
 //                  render.hip (< 0; b == a for a one-primitive leaf);
 //     empty slot:  an empty box (min = +inf, max = -inf), never entered.
-//   An inner child's box is stored grown by `inflate` (render.hip passes 2^-19 x
-//   the scene's largest coordinate): a computed primitive hit lies outside its
-//   box by a few ulps of the coordinates, and growing the box in space grows
+//   An inner child's box is stored grown by `inflate` x its own largest
+//   |coordinate| (render.hip passes 2^-19): a computed primitive hit lies outside
+//   its box by a few ulps of the coordinates, and growing the box in space grows
 //   each axis's t interval by that distance x |1/d_k| - the right slack for a
 //   ray (nearly) parallel to a box face, at no cost per node (DESIGN.md §3
 //   "Grazing rays").
@@ -285,10 +285,13 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
         } else {
           ref = pos[size_t(wide_of[c])];
           ref_b = 0;
-          for (int a = 0; a < 3 && inflate > 0.0f; ++a) {  // grown outward, rounded outward
-            float lo = box.mn[a] - inflate, hi = box.mx[a] + inflate;
-            if (double(lo) > double(box.mn[a]) - double(inflate)) lo = std::nextafter(lo, -INFINITY);
-            if (double(hi) < double(box.mx[a]) + double(inflate)) hi = std::nextafter(hi, INFINITY);
+          double cmax = 0.0;
+          for (int a = 0; a < 3; ++a) cmax = std::max({cmax, std::fabs(double(box.mn[a])), std::fabs(double(box.mx[a]))});
+          const double g = double(inflate) * cmax;
+          for (int a = 0; a < 3 && g > 0.0; ++a) {  // grown outward, rounded outward
+            float lo = float(double(box.mn[a]) - g), hi = float(double(box.mx[a]) + g);
+            if (double(lo) > double(box.mn[a]) - g) lo = std::nextafter(lo, -INFINITY);
+            if (double(hi) < double(box.mx[a]) + g) hi = std::nextafter(hi, INFINITY);
             box.mn[a] = lo;
             box.mx[a] = hi;
           }

@@ -23,8 +23,9 @@ struct WideBvh {
 };
 
 // top_levels: how many levels (root = 1) are stored first, breadth-first.
-// inflate: inner children's boxes are stored grown by this much on every side
-// (rounded outward); leaf children keep the reference leaf's box bit for bit.
+// inflate: inner children's boxes are stored grown on every side by this much
+// times their own largest |coordinate| (rounded outward); leaf children keep
+// the reference leaf's box bit for bit.
 WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels = 2, float inflate = 0.0f);
 
 }  // namespace zrt

@@ -107,7 +107,7 @@ struct KArgs {
   uint32_t n_mats, mats_in_lds;
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
-  float scene_extent;     // max |coordinate| of the primitives' boxes (RayT::slack)
+  float scene_extent;     // the triangles' largest |coordinate| (RayT::slack)
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -327,46 +327,50 @@ struct RayT {
   // wave-uniform value (from KArgs), so the choice below is a scalar branch
   uint32_t rcp_det;
   // absolute slacks in t of the narrowed culls (ray_slack): entry > exit * (1 + 2^-16) + slack culls
-  float slack;      // reference boxes (leaf slots, BINARY, the replay)
-  float slack_far;  // inner wide slots (boxes stored grown): 0 unless |o| exceeds the scene extent
+  float slack;  // reference boxes (leaf slots, BINARY, the replay)
+  float rel;    // relative margin of every narrowed cull: 1 + 2^-16 + 2^-18 max_k |1/d_k|
 };
 
-// A computed primitive hit lies outside its own box by a few ulps of the
-// coordinates involved (up to 4e-6 x max(scene extent, |o|) on the rays of
-// tests/grazing_rays.py, most of it along the ray).  In t that is the distance
-// times |1/d_k| on the axis it is measured along, unbounded for a ray (nearly)
-// parallel to a box face: the relative margin alone culled boxes the reference
-// opens and hits in (DESIGN.md §3 "Grazing rays").  With delta = 2^-19 x
-// max(scene extent, |o|):
-// * inner wide slots: their boxes are stored grown by 2^-19 x scene extent
-//   (accel_build.cpp), which grows each axis's t interval by exactly that
-//   distance x |1/d_k|, per axis, at no cost per node; slack_far adds what a ray
-//   from beyond the scene extent needs on top (0 for every render ray);
-// * reference boxes (leaf slots, the BINARY traversal, the replay), which must
-//   stay bit for bit: a uniform slack 2 x delta x max_k |1/d_k|.  A leaf slot
-//   that fails the narrowed test by less goes through the reference's own loose
-//   test (loose_slot), which decides it exactly; an axis-parallel ray (slack
-//   inf) gets the loose test on every leaf slot of the nodes it visits.
-// On the grazing rays no hit lies outside its box's t interval by more than 0.27
-// of delta x M + 2^-16 t (tools/grazing_excess.py).
+// A computed primitive hit lies outside its own box: a triangle's by a few ulps
+// of the coordinates involved, about 2^-23 x (t + the triangle's largest
+// |coordinate|) (|o| <= t + that, so the origin adds nothing); a sphere's only
+// along the ray (its point is o + t d), i.e. by its error in t.  In t that is
+// the distance times |1/d_k| on the axis it is measured along, unbounded for a
+// ray (nearly) parallel to a box face: the relative margin alone culled boxes the
+// reference opens and hits in (DESIGN.md §3 "Grazing rays").  So:
+// * the t-proportional part: every narrowed cull's relative margin is
+//   1 + 2^-16 + 2^-18 max_k |1/d_k| (RayT::rel, per ray, no cost per node);
+// * the coordinate part, inner wide slots: their boxes are stored grown by
+//   2^-19 x their own largest |coordinate| (accel_build.cpp), which grows each
+//   axis's t interval by exactly that distance x |1/d_k|, at no cost per node;
+// * the coordinate part, reference boxes (leaf slots, the BINARY traversal, the
+//   replay), which stay bit for bit: a uniform slack 2^-18 x the triangles'
+//   largest |coordinate| x max_k |1/d_k| (RayT::slack).  A leaf slot failing the
+//   narrowed test by less is decided by loose_slot: the reference's own
+//   per-axis test, and the narrowed test of the leaf's box grown by its own
+//   coordinates.
+// On the grazing rays no hit lies outside its box's t interval by more than 0.72
+// of half these margins (tools/grazing_excess.py).
 #ifndef ZRT_GRAZE_SLACK
 #define ZRT_GRAZE_SLACK 1  // 0: A/B only (round-2 margins, not exact on grazing rays)
 #endif
 #ifndef ZRT_GROW
 #define ZRT_GROW ZRT_GRAZE_SLACK  // A/B only: 0 stores inner boxes ungrown (not exact)
 #endif
+#ifndef ZRT_REL_M
+#define ZRT_REL_M ZRT_GRAZE_SLACK  // A/B only: 0 keeps the constant relative margin (not exact)
+#endif
 #ifndef ZRT_LEAF_SLACK
 #define ZRT_LEAF_SLACK ZRT_GRAZE_SLACK  // A/B only: 0 drops the leaf slots' slack (not exact)
 #endif
 __device__ __forceinline__ void ray_slack(float scene_extent, RayT& r) {
-  r.slack = r.slack_far = 0.0f;
+  r.slack = 0.0f;
+  r.rel = 1.0000153f;
   if (!ZRT_GRAZE_SLACK) return;
-  const float om = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox), __builtin_fabsf(r.oy)),
-                                   __builtin_fabsf(r.oz));
   const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ix), __builtin_fabsf(r.iy)),
                                   __builtin_fabsf(r.iz));
-  r.slack = __builtin_fmaxf(__builtin_fmaxf(scene_extent, om), 0x1p-100f) * 0x1p-18f * m;
-  if (om > scene_extent) r.slack_far = (om - scene_extent) * 0x1p-18f * m;
+  r.slack = ZRT_LEAF_SLACK ? __builtin_fmaxf(scene_extent, 0x1p-100f) * 0x1p-18f * m : 0.0f;
+  r.rel = ZRT_REL_M ? 1.0000153f + 0x1p-18f * m : 1.0000153f;
 }
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
@@ -393,7 +397,7 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && !(en > __builtin_fmaf(ex, 1.0000153f, r.slack));
+    ok = ok && !(en > __builtin_fmaf(ex, r.rel, r.slack));
     *entry = en;
   }
   return ok;
@@ -775,7 +779,7 @@ __device__ __forceinline__ float wide_slot(float mnx, float mny, float mnz, floa
   const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, tb);
   const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
   const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-  bool ok = !(en > __builtin_fmaf(ex, 1.0000153f, r.slack));
+  bool ok = !(en > __builtin_fmaf(ex, r.rel, r.slack));
   if (leaf) ok = ok && (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) per axis
   return ok ? en : __builtin_inff();
 }
@@ -828,9 +832,26 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   const float nx = (f[px] - r.ox) * r.ix, fx = (f[qx] - r.ox) * r.ix;
   const float ny = (f[py] - r.oy) * r.iy, fy = (f[qy] - r.oy) * r.iy;
   const float nz = (f[pz] - r.oz) * r.iz, fz = (f[qz] - r.oz) * r.iz;
-  return (__builtin_fminf(fx, tb) > __builtin_fmaxf(nx, t_min)) &&
-         (__builtin_fminf(fy, tb) > __builtin_fmaxf(ny, t_min)) &&
-         (__builtin_fminf(fz, tb) > __builtin_fmaxf(nz, t_min));
+  if (!ZRT_GRAZE_SLACK)
+    return (__builtin_fminf(fx, tb) > __builtin_fmaxf(nx, t_min)) &&
+           (__builtin_fminf(fy, tb) > __builtin_fmaxf(ny, t_min)) &&
+           (__builtin_fminf(fz, tb) > __builtin_fmaxf(nz, t_min));
+  // the leaf's own coordinate slack (ray_slack): g = 2 x 2^-19 x its largest |coordinate|,
+  // g |1/d_k| on axis k; a hit below the leaf's entry by that still counts against tb
+  const float cl = __builtin_fmaxf(
+      __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(f[px]), __builtin_fabsf(f[qx])),
+                      __builtin_fmaxf(__builtin_fabsf(f[py]), __builtin_fabsf(f[qy]))),
+      __builtin_fmaxf(__builtin_fabsf(f[pz]), __builtin_fabsf(f[qz])));
+  const float g = cl * 0x1p-18f;
+  const float gx = g * __builtin_fabsf(r.ix), gy = g * __builtin_fabsf(r.iy), gz = g * __builtin_fabsf(r.iz);
+  const float tl = tb + __builtin_fmaxf(__builtin_fmaxf(gx, gy), gz);
+  const bool loose = (__builtin_fminf(fx, tl) > __builtin_fmaxf(nx, t_min)) &&
+                     (__builtin_fminf(fy, tl) > __builtin_fmaxf(ny, t_min)) &&
+                     (__builtin_fminf(fz, tl) > __builtin_fmaxf(nz, t_min));
+  // the narrowed test of the box grown by g (NaN bounds constrain nothing)
+  const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
+  const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
+  return loose && !(en > ex * r.rel);
 }
 
 constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
@@ -975,12 +996,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
   const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
   const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
-  // narrowed test: entry > exit * (1 + 2^-16) + slack culls (ray_slack: inner
-  // slots' boxes are stored grown, leaf slots' are the reference leaves')
-  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, 1.0000153f, r0 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
-  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, 1.0000153f, r1 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
-  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, 1.0000153f, r2 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
-  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, 1.0000153f, r3 < 0 && ZRT_LEAF_SLACK ? r.slack : r.slack_far));
+  // narrowed test: entry > exit * rel (+ slack for a leaf slot) culls (ray_slack:
+  // inner slots' boxes are stored grown, leaf slots' are the reference leaves')
+  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, r.rel, r0 < 0 ? r.slack : 0.0f));
+  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, r.rel, r1 < 0 ? r.slack : 0.0f));
+  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, r.rel, r2 < 0 ? r.slack : 0.0f));
+  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, r.rel, r3 < 0 ? r.slack : 0.0f));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
@@ -990,12 +1011,10 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
   const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-    // (a hit may lie below its leaf's entry by the slack: loose test against tb + slack)
-    const float tl = tb + r.slack;
-    if (w0) o0 = loose_slot(q, 0, r, tl, sx, sy, sz);
-    if (w1) o1 = loose_slot(q, 1, r, tl, sx, sy, sz);
-    if (w2) o2 = loose_slot(q, 2, r, tl, sx, sy, sz);
-    if (w3) o3 = loose_slot(q, 3, r, tl, sx, sy, sz);
+    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
+    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
+    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
+    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
   }
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
   const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
@@ -2376,11 +2395,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
     const double tw = now_ms();
-    // the scene's largest coordinate (leaf boxes are unions of the primitives' boxes)
-    for (const RefLeaf& L : leaves)
-      for (int k = 0; k < 3; ++k)
-        c->scene_extent = std::max({c->scene_extent, std::fabs(L.mn[k]), std::fabs(L.mx[k])});
-    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? std::ldexp(c->scene_extent, -19) : 0.0f);
+    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
@@ -2412,14 +2427,9 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   std::vector<float4> shade(slot_to_prim.size());
   for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
     const zrt_prim& p = s->prims[slot_to_prim[sl]];
-    if (p.kind == ZRT_PRIM_TRIANGLE) {
+    if (p.kind == ZRT_PRIM_TRIANGLE)  // RayT::slack: the triangles' largest |coordinate|
       for (const auto& v : {p.a, p.b, p.c})
         c->scene_extent = std::max({c->scene_extent, std::fabs(v.x), std::fabs(v.y), std::fabs(v.z)});
-    } else {
-      c->scene_extent = std::max({c->scene_extent, std::fabs(p.center.x) + std::fabs(p.radius),
-                                  std::fabs(p.center.y) + std::fabs(p.radius),
-                                  std::fabs(p.center.z) + std::fabs(p.radius)});
-    }
     float4* q = &prims[3 * sl];
     float4& sh = shade[sl];
     uint32_t tag = p.material;
