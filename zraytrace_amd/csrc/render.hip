@@ -107,7 +107,7 @@ struct KArgs {
   uint32_t n_mats, mats_in_lds;
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
-  float scene_extent;     // the triangles' largest |coordinate| (RayT::slack)
+  float scene_extent;     // the triangles' largest |coordinate| (ray_slack)
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -326,9 +326,6 @@ struct RayT {
   // triangle.zig:61 that passes det >= 1e-6 lies in dev::rcp_core's range; a
   // wave-uniform value (from KArgs), so the choice below is a scalar branch
   uint32_t rcp_det;
-  // absolute slacks in t of the narrowed culls (ray_slack): entry > exit * (1 + 2^-16) + slack culls
-  float slack;  // reference boxes (leaf slots, BINARY, the replay)
-  float rel;    // relative margin of every narrowed cull: 1 + 2^-16 + 2^-18 max_k |1/d_k|
 };
 
 // A computed primitive hit lies outside its own box: a triangle's by a few ulps
@@ -339,13 +336,13 @@ struct RayT {
 // ray (nearly) parallel to a box face: the relative margin alone culled boxes the
 // reference opens and hits in (DESIGN.md §3 "Grazing rays").  So:
 // * the t-proportional part: every narrowed cull's relative margin is
-//   1 + 2^-16 + 2^-18 max_k |1/d_k| (RayT::rel, per ray, no cost per node);
+//   1 + 2^-16 + 2^-18 max_k |1/d_k| (ray_rel, per ray);
 // * the coordinate part, inner wide slots: their boxes are stored grown by
 //   2^-19 x their own largest |coordinate| (accel_build.cpp), which grows each
 //   axis's t interval by exactly that distance x |1/d_k|, at no cost per node;
 // * the coordinate part, reference boxes (leaf slots, the BINARY traversal, the
 //   replay), which stay bit for bit: a uniform slack 2^-18 x the triangles'
-//   largest |coordinate| x max_k |1/d_k| (RayT::slack).  A leaf slot failing the
+//   largest |coordinate| x max_k |1/d_k| (ray_slack).  A leaf slot failing the
 //   narrowed test by less is decided by loose_slot: the reference's own
 //   per-axis test, and the narrowed test of the leaf's box grown by its own
 //   coordinates.
@@ -363,14 +360,16 @@ struct RayT {
 #ifndef ZRT_LEAF_SLACK
 #define ZRT_LEAF_SLACK ZRT_GRAZE_SLACK  // A/B only: 0 drops the leaf slots' slack (not exact)
 #endif
-__device__ __forceinline__ void ray_slack(float scene_extent, RayT& r) {
-  r.slack = 0.0f;
-  r.rel = 1.0000153f;
-  if (!ZRT_GRAZE_SLACK) return;
-  const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ix), __builtin_fabsf(r.iy)),
-                                  __builtin_fabsf(r.iz));
-  r.slack = ZRT_LEAF_SLACK ? __builtin_fmaxf(scene_extent, 0x1p-100f) * 0x1p-18f * m : 0.0f;
-  r.rel = ZRT_REL_M ? 1.0000153f + 0x1p-18f * m : 1.0000153f;
+// (recomputed where used from 1/d, 1 VALU each, rather than kept in VGPRs across
+// the traversal: two more live registers cost the deep-tree loop spills)
+__device__ __forceinline__ float ray_m(const RayT& r) {  // max_k |1/d_k|
+  return __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ix), __builtin_fabsf(r.iy)), __builtin_fabsf(r.iz));
+}
+// relative margin of every narrowed cull: 1 + 2^-16 + 2^-18 m
+__device__ __forceinline__ float ray_rel(float m) { return ZRT_REL_M ? 1.0000153f + 0x1p-18f * m : 1.0000153f; }
+// the reference boxes' slack: 2^-18 x the triangles' largest |coordinate| x m
+__device__ __forceinline__ float ray_slack(float extent, float m) {
+  return ZRT_LEAF_SLACK ? __builtin_fmaxf(extent, 0x1p-100f) * 0x1p-18f * m : 0.0f;
 }
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
@@ -378,7 +377,7 @@ __device__ __forceinline__ void ray_slack(float scene_extent, RayT& r) {
 // margin) and reports the entry distance for near-first ordering.
 template <bool FAST>
 __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const RayT& r, float t_max,
-                                         float* entry) {
+                                         float* entry, float slack = 0.0f) {
   const float t_min = 0.001f;
   float a0 = (lo.x - r.ox) * r.ix, a1 = (hi.x - r.ox) * r.ix;
   float b0 = (lo.y - r.oy) * r.iy, b1 = (hi.y - r.oy) * r.iy;
@@ -397,7 +396,7 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && !(en > __builtin_fmaf(ex, r.rel, r.slack));
+    ok = ok && !(en > __builtin_fmaf(ex, ray_rel(ray_m(r)), slack));
     *entry = en;
   }
   return ok;
@@ -635,6 +634,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
                                               float& best_t, int& best) {
   const uint32_t rows = a.lds_rows, cap = a.ref_stack;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
+  const float slack = ray_slack(a.scene_extent, ray_m(r));
   best_t = __builtin_inff();
   best = -1;
   uint32_t c_tri = 0, c_sph = 0;
@@ -649,7 +649,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
     // emptiness test (a box the ray does not cross holds no hit):
     // left-first with the reference's t_max, so every leaf is accepted or
     // rejected exactly as the reference does it, in ~1 % of its node visits
-    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e)) continue;
+    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e, slack)) continue;
     const int left = as_int(lo.w), right = as_int(hi.w);
     if (left < 0) {
       prim_test<false, false>(a.prims, left, r, best_t, best, c_tri, c_sph);
@@ -679,10 +679,11 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
   uint32_t sp = 0;
   const uint32_t cap = a.stack_depth;
   if (FAST) {
+    const float slack = ray_slack(a.scene_extent, ray_m(r));
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
-    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * kOpen + r.slack, &e)) return;
+    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) return;
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
@@ -692,10 +693,10 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const float4 l0 = a.nodes[2 * left], l1 = a.nodes[2 * left + 1];
         const float4 r0 = a.nodes[2 * right], r1 = a.nodes[2 * right + 1];
         if (STATS) c_nodes += 2;
-        const float tb = __builtin_fabsf(best_t) * kOpen + r.slack;
+        const float tb = __builtin_fabsf(best_t) * kOpen + slack;
         float el, er;
-        const bool hl = box_test<true>(l0, l1, r, tb, &el);
-        const bool hr = box_test<true>(r0, r1, r, tb, &er);
+        const bool hl = box_test<true>(l0, l1, r, tb, &el, slack);
+        const bool hr = box_test<true>(r0, r1, r, tb, &er, slack);
         if (hl && hr) {
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
@@ -715,7 +716,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const int idx = stk[sp * stride];
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
-        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * kOpen + r.slack, &e)) {
+        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
           found = true;
@@ -779,7 +780,7 @@ __device__ __forceinline__ float wide_slot(float mnx, float mny, float mnz, floa
   const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, tb);
   const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
   const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-  bool ok = !(en > __builtin_fmaf(ex, r.rel, r.slack));
+  bool ok = !(en > ex * ray_rel(ray_m(r)));
   if (leaf) ok = ok && (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) per axis
   return ok ? en : __builtin_inff();
 }
@@ -851,7 +852,7 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   // the narrowed test of the box grown by g (NaN bounds constrain nothing)
   const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
   const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
-  return loose && !(en > ex * r.rel);
+  return loose && !(en > ex * ray_rel(ray_m(r)));
 }
 
 constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
@@ -980,6 +981,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool sx = v.sx, sy = v.sy, sz = v.sz;
   int r0 = as_int(w.ra.x), r1 = as_int(w.ra.y), r2 = as_int(w.ra.z), r3 = as_int(w.ra.w);
   const float tb = __builtin_fabsf(best_t) * kOpen;
+  const float m = ray_m(r), rel = ray_rel(m), slk = ray_slack(a.scene_extent, m);
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
@@ -998,10 +1000,10 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
   // narrowed test: entry > exit * rel (+ slack for a leaf slot) culls (ray_slack:
   // inner slots' boxes are stored grown, leaf slots' are the reference leaves')
-  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, r.rel, r0 < 0 ? r.slack : 0.0f));
-  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, r.rel, r1 < 0 ? r.slack : 0.0f));
-  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, r.rel, r2 < 0 ? r.slack : 0.0f));
-  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, r.rel, r3 < 0 ? r.slack : 0.0f));
+  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, rel, r0 < 0 ? slk : 0.0f));
+  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, rel, r1 < 0 ? slk : 0.0f));
+  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, rel, r2 < 0 ? slk : 0.0f));
+  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, rel, r3 < 0 ? slk : 0.0f));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
@@ -1584,8 +1586,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
       r.rcp_det = a.tri_rcp_fast;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
-      ray_slack(a.scene_extent, r);
-      float best_t = __builtin_inff();
+            float best_t = __builtin_inff();
       int best = -1;
       if (MODE == 0) {
 #if ZRT_LIST_SCALAR && defined(__HIP_DEVICE_COMPILE__)
@@ -1858,8 +1859,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     r.ox = o.x; r.oy = o.y; r.oz = o.z;
     r.dx = d.x; r.dy = d.y; r.dz = d.z;
     inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
-    ray_slack(a.scene_extent, r);
-    best_t = __builtin_inff();
+        best_t = __builtin_inff();
     best = -1;
     sp = 0;
     {
@@ -1933,8 +1933,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
   r.rcp_det = a.tri_rcp_fast;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
-  ray_slack(a.scene_extent, r);
-  float best_t = __builtin_inff();
+    float best_t = __builtin_inff();
   int best = -1;
   uint32_t c_nodes = 0, c_leaves = 0, c_tri = 0, c_sph = 0;
   if (MODE == 0) {
@@ -2427,7 +2426,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   std::vector<float4> shade(slot_to_prim.size());
   for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
     const zrt_prim& p = s->prims[slot_to_prim[sl]];
-    if (p.kind == ZRT_PRIM_TRIANGLE)  // RayT::slack: the triangles' largest |coordinate|
+    if (p.kind == ZRT_PRIM_TRIANGLE)  // ray_slack: the triangles' largest |coordinate|
       for (const auto& v : {p.a, p.b, p.c})
         c->scene_extent = std::max({c->scene_extent, std::fabs(v.x), std::fabs(v.y), std::fabs(v.z)});
     float4* q = &prims[3 * sl];
