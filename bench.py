@@ -62,32 +62,53 @@ def algorithmic_bytes(st, n_work_units, n_pixels):
             + (st["texel_bytes"] or 12) * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 
-def pmc_entry(config):
-    """The PMC record of render_kernel for this exact config (profiles/latest_pmc.json,
-    written by tools/make_latest_pmc.py from rocprofv3 --pmc passes); None if not measured."""
+def pmc_entry(config, build_id):
+    """(entry, reason): the PMC record of render_kernel for this exact config AND
+    this exact kernel build (profiles/latest_pmc.json, written by
+    tools/make_latest_pmc.py from rocprofv3 --pmc passes, keyed by
+    zrt_build_id()); (None, why) when there is none, so counters of another
+    build are never attached to this one."""
     try:
         with open(os.path.join(REPO, "profiles", "latest_pmc.json")) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "profiles/latest_pmc.json missing"
+    stale = None
     for e in d.get("entries", []):
-        if e.get("config") == config:
-            return e
-    return None
+        if e.get("config") != config:
+            continue
+        if e.get("build_id") == build_id:
+            return e, None
+        stale = e.get("build_id")
+    if stale is not None:
+        return None, f"PMC entry for this config was taken on build {stale}, this library is {build_id}"
+    return None, "no PMC entry for this config"
+
+
+# The guide's architectural issue rate: one wave64 VALU instruction per 2 cycles
+# per SIMD (MI355X_MICROARCH.md).  tools/ubench.hip's single-kernel measurement
+# (profiles/ubench.json) reached 0.419 of a cycle, i.e. 84 % of it; the roofline
+# prices against the architectural figure and reports the measured one beside it.
+VALU_ISSUE_PER_SIMD_CLK = 0.5
 
 
 def ubench_peaks():
     """Per-clock ceilings measured by tools/ubench.hip under rocprofv3 on the GPU box
-    (profiles/ubench.json, tools/gpu_ubench.sh); the guide's figures where absent."""
+    (profiles/ubench.json, tools/gpu_ubench.sh); the guide's figures where absent.
+    VALU issue is always the guide's architectural rate (VALU_ISSUE_PER_SIMD_CLK)."""
     try:
         with open(os.path.join(REPO, "profiles", "ubench.json")) as f:
-            return json.load(f)["peaks_per_clock"], "profiles/ubench.json (tools/ubench.hip, rocprofv3 --pmc)"
+            p = dict(json.load(f)["peaks_per_clock"])
+        src = "profiles/ubench.json (tools/ubench.hip, rocprofv3 --pmc)"
     except (OSError, ValueError, KeyError):
-        return ({"valu_insts_per_simd": 0.5, "tcp_accesses_per_cu": 1.0, "l2_read_req_per_cu": 0.375},
-                "MI355X_MICROARCH.md (one wave64 VALU per 2 cycles per SIMD; 64 B/clk/CU L1; L2 34.5 TB/s)")
+        p = {"tcp_accesses_per_cu": 1.0, "l2_read_req_per_cu": 0.375}
+        src = "MI355X_MICROARCH.md (64 B/clk/CU L1; L2 34.5 TB/s)"
+    p["valu_measured_per_simd"] = p.get("valu_insts_per_simd")
+    p["valu_insts_per_simd"] = VALU_ISSUE_PER_SIMD_CLK
+    return p, src + "; VALU issue: MI355X_MICROARCH.md, 0.5 wave64 inst/SIMD/clk"
 
 
-def roofline(pmc, kernel_s, algo_bytes, diag):
+def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None):
     """The render launch against every ceiling it could be bound by.  Per ceiling:
     the PMC count per launch (rocprofv3 pass of this exact config) / the launch's
     HIP-event time measured in this run = achieved, against the measured per-clock
@@ -100,6 +121,8 @@ def roofline(pmc, kernel_s, algo_bytes, diag):
     bound = the ceiling with the largest fraction."""
     out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
            "kernel_s": round(kernel_s, 6)}
+    if not pmc:
+        out["reason"] = pmc_reason
     rows = {}
     if pmc:
         peaks, src = ubench_peaks()
@@ -125,12 +148,17 @@ def roofline(pmc, kernel_s, algo_bytes, diag):
         out["traffic"] = pmc.get("hbm_bytes_per_launch")
         out["pmc_source"] = pmc.get("source")
         out["valu_lane_util"] = sq.get("valu_lane_util")
+        out["pmc_build_id"] = pmc.get("build_id")
         if cache.get("TCC_HIT_sum") is not None and cache.get("TCC_MISS_sum"):
             out["l2_hit_frac"] = round(cache["TCC_HIT_sum"] / (cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"]), 4)
     if rows:
         b = max(rows, key=lambda k: rows[k]["frac"])
         out.update({"bound": b, "achieved": rows[b]["achieved"], "peak": rows[b]["peak"], "unit": rows[b]["unit"],
                     "frac": rows[b]["frac"]})
+        if "valu_issue" in rows and out.get("valu_lane_util"):
+            # issue fraction x active-lane fraction: the share of the chip's VALU lane slots doing work
+            rows["valu_issue"]["useful_lane_frac"] = round(rows["valu_issue"]["frac"] * out["valu_lane_util"], 4)
+            rows["valu_issue"]["measured_peak_per_simd_clk"] = peaks.get("valu_measured_per_simd")
         if "hbm" in rows:
             out["hbm_gbs_measured"] = round(rows["hbm"]["achieved"] / 1e9, 1)
             out["hbm_frac"] = rows["hbm"]["frac"]
@@ -145,6 +173,21 @@ def roofline(pmc, kernel_s, algo_bytes, diag):
                     "prim_tests": round(diag["prim_tests"] / rays, 2),
                     "bytes": round(algo_bytes / rays, 1)}}
     return out
+
+
+def n1_frame_hash(config):
+    """The committed frame hash of this config rendered on ONE GPU
+    (profiles/frame_hashes.json); an N-rank frame must equal it bit for bit
+    (the image is independent of the partition).  None if absent."""
+    try:
+        with open(os.path.join(REPO, "profiles", "frame_hashes.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for e in d.get("entries", []):
+        if e.get("config") == config:
+            return e.get("frame_sha1")
+    return None
 
 
 def cpu_model():
@@ -275,6 +318,8 @@ def main():
     elapsed = time.perf_counter() - t0
 
     st = fr.ctx.stats()  # Progress counters of the last timed launch (identical every step)
+    # per-rank kernel and gather times of the timed steps (HIP events on the frame's stream)
+    my_times = [sum(kernel_ms) / len(kernel_ms), sum(fr.gather_ms) / max(1, len(fr.gather_ms))]
     frame_sha1 = hashlib.sha1(fr.image().tobytes()).hexdigest() if rank == 0 else None
     # Traffic diagnostics (node visits, primitive tests, ...) come from one extra,
     # untimed launch of the diagnostic kernel flavour: same traversal, same image.
@@ -290,6 +335,12 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     total_rays, total_samples = rays.tolist()
     elapsed = el.item()
+    per_rank = [my_times]
+    if world > 1:
+        tt = torch.tensor(my_times, dtype=torch.float64, device=red)
+        allt = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(allt, tt)
+        per_rank = [x.tolist() for x in allt]
 
     if rank == 0:
         value = total_rays * args.steps / elapsed / 1e6
@@ -299,7 +350,14 @@ def main():
         algo = algorithmic_bytes(diag, n_units, diag["pixels_processed"])
         pmc_key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                    "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
-        roof = roofline(pmc_entry(pmc_key) if world == 1 else None, avg_kernel_s, algo, diag)
+        bid = z.build_id()
+        if world == 1:
+            pe, why = pmc_entry(pmc_key, bid)
+        else:
+            pe, why = None, "PMC passes are taken at N=1 only"
+        if bid.split("-")[0] != z.build_id_of_sources():
+            pe, why = None, f"libzrt.so ({bid}) is stale against its sources ({z.build_id_of_sources()})"
+        roof = roofline(pe, avg_kernel_s, algo, diag, why)
         # what the render launch writes to memory: each work unit's
         # 64 chunk sums (float4), the attenuation rows past the LDS ones (float4; STATS
         # counter kAttWrites of the diagnostic launch) and, on deep trees, the traversal
@@ -308,10 +366,18 @@ def main():
         wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 16 * int(dc[28]),
               "stack_rows_B": 4 * int(dc[30])}  # FAST stack entries past the LDS rows (kStackOvfWrites)
         wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
-        pe = pmc_entry(pmc_key) if world == 1 else None
         if pe and pe.get("write_size_kb"):
             wb["pmc_write_B"] = int(pe["write_size_kb"] * 1024)
             wb["predicted_over_pmc"] = round(wb["predicted_B"] / wb["pmc_write_B"], 3)
+            c = pe.get("cache") or {}
+            if c.get("TCC_EA0_WRREQ_sum"):
+                # L2 -> memory write requests: 64-B (whole line) and 32-B (partial) ones;
+                # WRITE_SIZE = 64 x WRREQ_64B + 32 x the rest on gfx950
+                n64 = c.get("TCC_EA0_WRREQ_64B_sum", 0.0)
+                n32 = c["TCC_EA0_WRREQ_sum"] - n64
+                wb["pmc_wrreq_64B"] = int(n64)
+                wb["pmc_wrreq_32B"] = int(n32)
+                wb["pmc_wrreq_bytes"] = int(64 * n64 + 32 * n32)
         roof["write_budget"] = wb
         roof["kernel"] = f"render_kernel (BVH {args.traversal} traversal)"
         roof["counters_from"] = f"one untimed ZRT_FLAG_STATS launch (kernel {diag_kernel_ms:.1f} ms)"
@@ -345,7 +411,13 @@ def main():
                       "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
             "frame_sha1": frame_sha1,
+            "build_id": bid,
+            "per_rank_ms": {"kernel": [round(x[0], 3) for x in per_rank],
+                            "gather": [round(x[1], 3) for x in per_rank]},
         }
+        ref_hash = n1_frame_hash(pmc_key)
+        out["frame_sha1_n1"] = ref_hash
+        out["frame_equal_to_n1"] = (frame_sha1 == ref_hash) if ref_hash else None
         if world == 1 and args.traversal == "fast" and st["used_bvh"] and not args.no_reference_check:
             if scene.n_prims <= 100_000:
                 log("[rank 0] reference-traversal launch of the same frame ...")

@@ -303,6 +303,10 @@ const char* zrt_last_error(void);
 /* ABI version (ZRT_ABI_VERSION) and build identity string. */
 int zrt_abi_version(void);
 const char* zrt_build_info(void);
+/* What the kernels of this library were built from: sha1 of the device and
+ * tree-layout sources + zrt.h (16 hex digits) - sha1 of the device compile
+ * flags (8).  Performance-counter records are keyed by it (bench.py). */
+const char* zrt_build_id(void);
 
 /* ---- device-resident context (bench / multi-GPU) ------------------------ *
  * zrt_ctx_create does preprocessSufraces (BVH build, raytrace.zig:124-133),

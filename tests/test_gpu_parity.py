@@ -171,6 +171,46 @@ def test_c5_substitute_bit_exact(scenes):
             assert gs[k] == rs[k], k
 
 
+@pytest.mark.parametrize("loop,rows", [("wavefront", None), ("wavefront", "2"), ("lockstep", "2")])
+def test_c5_substitute_depth20_vs_golden(scenes, loop, rows, monkeypatch):
+    """the C5 path at its real depth.  Scene 6 at 32x32 x 2 spp,
+    max depth 20, 1-sample chunks, against the oracle's frame, progress counters
+    and per-scanline counters (tests/golden/c5_depth20.npz, made by
+    tests/golden/make_c5_golden.py: the oracle needs ~160 s for it).  The
+    wavefront loop (the C5 default) and the lockstep loop; rows="2" forces the
+    FAST stack onto its global rows past 2 LDS rows, and every run keeps no
+    attenuation row in LDS (ZRT_ATT_LDS_ROWS=0), so both deep-tree paths to
+    global memory are taken - checked with the STATS counters kAttWrites and
+    kStackOvfWrites."""
+    import os
+    import torch
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_depth20.npz"))
+    w, h, spp, depth, chunk = (int(x) for x in g["params"])
+    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    monkeypatch.setenv("ZRT_ATT_LDS_ROWS", "0")
+    if rows:
+        monkeypatch.setenv("ZRT_STACK_LDS_ROWS", rows)
+    s = scenes(6)
+    p = z.RenderParams(w, h, spp, depth, sample_chunk=chunk)
+    gpu, gs, grows = z.render_progress(s, s.camera, p)
+    assert_bit_exact(gpu, g["image"])
+    for name, v in zip(g["counter_names"], g["counters"]):
+        assert gs[str(name)] == int(v), name
+    np.testing.assert_array_equal(grows, g["rows"])
+    assert gs["reflections"] > 0 and gs["recursion_depth_hits"] >= 0
+    # the same frame from a context, diagnostic flavour: rows past LDS were used
+    ctx = z.RenderContext(s, p)
+    buf = torch.zeros(ctx.tile_count(p) * 64 * 3, dtype=torch.float32, device="cuda")
+    ps = z.RenderParams(**{**p.__dict__, "flags": z.ZRT_FLAG_STATS})
+    ctx.render_tiles(s.camera, ps, buf.data_ptr())
+    ctx.sync()
+    dc = ctx.debug_counters(32)
+    assert dc[28] > 0, "no attenuation row reached global memory"  # kAttWrites
+    if rows:
+        assert dc[30] > 0, "no stack entry reached the global rows"  # kStackOvfWrites
+    ctx.close()
+
+
 def test_nonsquare_and_ragged_tiles(scenes):
     """height < width: raytrace.zig:168 leaves columns x >= height black; 8x8
     tiles overhang both edges (37 x 21)."""

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import zraytrace_amd as z
+from zraytrace_amd import _ffi
 from oracle import oracle_py as O
 
 pytestmark = pytest.mark.gpu
@@ -287,3 +288,22 @@ def test_device_bvh_c5_substitute(scenes):
     assert (len(d[0]), d[4]) == (1894803, 39)
     print(f"device build {t1 - t0:.3f} s, host build {t2 - t1:.3f} s")
     assert t1 - t0 < (t2 - t1) / 3
+
+
+def test_device_bvh_failure_falls_back_to_host(scenes, monkeypatch):
+    """a HIP failure inside the device BVH build (forced here with
+    ZRT_DEBUG_BVH_DEVICE_FAIL) makes zrt_bvh_build_device fail with ZRT_E_HIP,
+    while zrt_render falls back to the host build of the same tree: the frame
+    and counters equal those of a host-built context."""
+    s = scenes(2)
+    p = z.RenderParams(24, 24, 2, 8)
+    monkeypatch.setenv("ZRT_BVH_DEVICE", "0")
+    ref, rst = z.render(s, s.camera, p)
+    monkeypatch.setenv("ZRT_BVH_DEVICE", "1")
+    monkeypatch.setenv("ZRT_DEBUG_BVH_DEVICE_FAIL", "1")
+    with pytest.raises(z.ZrtError) as e:
+        z.bvh_build_device(s)
+    assert e.value.code == _ffi.ZRT_E_HIP
+    img, st = z.render(s, s.camera, p)
+    assert (img.view(np.uint32) == ref.view(np.uint32)).all()
+    assert st["rays_processed"] == rst["rays_processed"]

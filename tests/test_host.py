@@ -243,8 +243,17 @@ def test_binary_scene_rejects(tmp_path):
     s = z.load_scene(1)
     good = tmp_path / "good.zrts"
     s.write(str(good))
-    (tmp_path / "cut.zrts").write_bytes(good.read_bytes()[:-100])
-    for p in (tmp_path / "cut.zrts", tmp_path / "missing.zrts"):
+    data = good.read_bytes()
+    (tmp_path / "cut.zrts").write_bytes(data[:-100])
+    # header counts from the file are checked against its size before
+    # anything is allocated (2^32 - 1 primitives would ask for 240 GB)
+    huge = bytearray(data)
+    huge[4 + 4 * 4: 4 + 4 * 5] = (0xFFFFFFFF).to_bytes(4, "little")  # head[4] = n_prims
+    (tmp_path / "huge.zrts").write_bytes(bytes(huge))
+    for name in ("cut.zrts", "huge.zrts"):
         with pytest.raises(z.ZrtError) as e:
-            z.LoadedScene.read(str(p))
-        assert e.value.code == _ffi.ZRT_E_IO
+            z.LoadedScene.read(str(tmp_path / name))
+        assert e.value.code == _ffi.ZRT_E_PARSE, name
+    with pytest.raises(z.ZrtError) as e:
+        z.LoadedScene.read(str(tmp_path / "missing.zrts"))
+    assert e.value.code == _ffi.ZRT_E_IO

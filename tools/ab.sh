@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG; mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
   for spec in "${VARS[@]}"; do
     v=${spec%%@*}; EXTRA_ARGS=(); [ "$spec" != "$v" ] && EXTRA_ARGS=(--chunk ${spec#*@})
-    if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/build/variants/$v/libzrt.so; fi
+    if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/abvar/$v/libzrt.so; fi
     ZRT_LIB=$LIB timeout -k 10 300 python $R/bench.py --no-cpu-baseline "$@" "${EXTRA_ARGS[@]}" > $OUT/$spec.$r.json 2> $OUT/$spec.$r.err || { echo "variant $v failed"; tail -5 $OUT/$spec.$r.err; exit 1; }
     python -c "import json,sys; d=json.load(open('$OUT/$spec.$r.json')); print('$spec', $r, d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['roofline']['algorithmic']['per_ray'])"
   done

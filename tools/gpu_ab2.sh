@@ -12,7 +12,7 @@ OUT=$R/gpurun_out/$TAG; mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
   for spec in "${SPECS[@]}"; do
     name=${spec%%=*}; rest=${spec#*=}; v=${rest%%:*}; envs=""; [ "$rest" != "$v" ] && envs=${rest#*:}
-    if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/build/variants/$v/libzrt.so; fi
+    if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/abvar/$v/libzrt.so; fi
     env ZRT_LIB=$LIB ${envs//,/ } timeout -k 10 300 python $R/bench.py --no-cpu-baseline --no-reference-check "$@" > $OUT/$name.$r.json 2> $OUT/$name.$r.err || { echo "variant $name failed"; tail -5 $OUT/$name.$r.err; exit 1; }
     python -c "import json; d=json.load(open('$OUT/$name.$r.json')); print('$name', $r, d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['frame_sha1'][:12])"
   done

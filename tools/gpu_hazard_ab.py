@@ -1,5 +1,5 @@
 """GPU box: FAST on tests/hazard_rays.py's adversarial rays with the library
-in ZRT_LIB (e.g. the round-1 opening margin, build/variants/open16) against the
+in ZRT_LIB (e.g. the round-1 opening margin, abvar/open16) against the
 oracle: how many hazard / band / order-effect rays it gets wrong."""
 import json
 import os

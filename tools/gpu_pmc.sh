@@ -17,7 +17,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES" \
            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE" \
-           "TCC_HIT_sum TCC_MISS_sum"; do
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
   i=$((i+1))
   timeout -s KILL 400 rocprofv3 --pmc $grp --output-format csv -d $O/pmc$i -o run -- python $B --steps 1 --warmup 0 > $O/pmc$i.json 2> $O/pmc$i.err || { echo "pmc pass $i ($grp) failed"; tail -3 $O/pmc$i.err; exit 1; }
 done

@@ -1,10 +1,14 @@
 # Rehearse bench.py's N>1 path on a one-GPU box: ranks share GPU 0 over gloo.
-# Compare frame_sha1 across the 1-, 2- and 3-rank lines: the frame must be identical.
+# Config C3 (scene 3, 1024x1024 @ 256 spp, depth 20): every line carries
+# frame_sha1 and frame_equal_to_n1 against the committed one-GPU hash
+# (profiles/frame_hashes.json) and per-rank kernel / gather milliseconds.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${1:-dist}; mkdir -p $O
 export MASTER_ADDR=127.0.0.1
-timeout -k 10 300 python $R/bench.py --width 1024 --height 1024 --spp 64 --no-cpu-baseline > $O/n1.json 2> $O/n1.err && tail -1 $O/n1.json && \
+A="--scene 3 --width 1024 --height 1024 --spp 256 --depth 20 --no-cpu-baseline"
+show() { python -c "import json; d=json.load(open('$1')); print(d['n_gpus'], d['value'], d['frame_sha1'][:12], d['frame_equal_to_n1'], d['per_rank_ms'])"; }
+timeout -k 10 300 python $R/bench.py $A > $O/n1.json 2> $O/n1.err && show $O/n1.json && \
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
-  $R/bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo --device 0 --width 1024 --height 1024 --spp 64 > $O/n2.json 2> $O/n2.err && tail -1 $O/n2.json && \
+  $R/bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo --device 0 $A > $O/n2.json 2> $O/n2.err && show $O/n2.json && \
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29518 \
-  $R/bench.py --gpus 3 --steps 2 --warmup 1 --dist-backend gloo --device 0 --width 1024 --height 1024 --spp 64 > $O/n3.json 2> $O/n3.err && tail -1 $O/n3.json
+  $R/bench.py --gpus 3 --steps 2 --warmup 1 --dist-backend gloo --device 0 $A > $O/n3.json 2> $O/n3.err && show $O/n3.json

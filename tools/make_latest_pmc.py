@@ -1,7 +1,8 @@
 """Merge a tools/pmc_summary.py entry into profiles/latest_pmc.json (read by bench.py).
 
 usage: python tools/make_latest_pmc.py <entry.json> <source label>
-An entry for the same config replaces the old one.
+An entry for the same config replaces the old one (bench.py attaches an entry
+only to a library whose zrt_build_id() equals the entry's build_id).
 """
 import json
 import os
@@ -15,6 +16,7 @@ def main():
     with open(src) as f:
         e = json.load(f)
     e["source"] = label
+    assert e.get("build_id"), "entry without build_id (bench line older than round 3?)"
     path = os.path.join(REPO, "profiles", "latest_pmc.json")
     try:
         with open(path) as f:

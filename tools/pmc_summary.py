@@ -10,8 +10,9 @@ diagnostic counters; the one-step run launches it once), and writes per launch:
   sq    - the SQ instruction counters and valu_lane_util
           = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU),
   cache - TCP (L1) accesses, L1->L2 read requests, TA / TD busy, GRBM_GUI_ACTIVE,
-          TCC (L2) hits / misses,
-and the bench config it was measured on (from <dir>/pmc1.json, bench's own line).
+          TCC (L2) hits / misses, L2 -> memory write requests (all / 64-B ones),
+and the bench config and zrt_build_id() it was measured on (from <dir>/pmc1.json,
+bench's own line): bench.py attaches the entry only to that config AND that build.
 """
 import csv
 import glob
@@ -45,7 +46,7 @@ def main():
     if sq.get("SQ_ACTIVE_INST_VALU"):
         sq["valu_lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]), 4)
     cache = {k: v for k, v in counters.items() if k.startswith(("TCP_", "TCC_", "TA_", "TD_", "GRBM_"))}
-    entry = {"config": cfg, "kernel": names.pop(),
+    entry = {"config": cfg, "build_id": bench.get("build_id"), "kernel": names.pop(),
              "hbm_bytes_per_launch": int((2 * counters["FETCH_SIZE"] + counters["WRITE_SIZE"]) * 1024),
              "fetch_size_kb": counters["FETCH_SIZE"], "write_size_kb": counters["WRITE_SIZE"],
              "duration_ns_per_pass": sorted(durations.values()),

@@ -1,5 +1,5 @@
 """Per-section cycle shares of the sampling loop (ZRT_PROFILE build; diagnostic).
-usage: ZRT_LIB=build/variants/prof/libzrt.so python tools/prof_sections.py [w h spp]"""
+usage: ZRT_LIB=abvar/prof/libzrt.so python tools/prof_sections.py [w h spp]"""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: F401  (shared HIP runtime)

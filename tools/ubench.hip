@@ -5,8 +5,8 @@
 // counters bench.py reads for render_kernel (SQ_INSTS_VALU,
 // TCP_TOTAL_CACHE_ACCESSES_sum, TCP_TCC_READ_REQ_sum) calibrate them.
 //
-// build: hipcc --offload-arch=gfx950 -O3 -o build/ubench tools/ubench.hip
-// run:   build/ubench > profiles/r02/ubench.json
+// build: hipcc --offload-arch=gfx950 -O3 -o abvar/ubench tools/ubench.hip
+// run:   abvar/ubench > profiles/r02/ubench.json
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

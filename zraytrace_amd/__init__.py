@@ -33,6 +33,31 @@ def lib():
     return _ffi.load()
 
 
+# csrc/Makefile ID_SRC, in its order, then include/zrt.h
+_ID_SRC = ("render.hip", "bvh_gpu.hip", "accel_build.cpp", "accel_build.hpp", "bvh_build.cpp", "bvh_build.hpp",
+           "device_math.hpp", "zrt.hpp")
+
+
+def build_id() -> str:
+    """zrt_build_id() of the loaded library: sha1 of the kernel sources (16 hex)
+    - sha1 of the device compile flags (8)."""
+    return lib().zrt_build_id().decode()
+
+
+def build_id_of_sources() -> str:
+    """The source half of zrt_build_id() recomputed from the files in the tree:
+    differs from build_id()'s when libzrt.so is stale against its sources."""
+    import hashlib
+    h = hashlib.sha1()
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    for f in _ID_SRC:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(REPO, "include", "zrt.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 @dataclass
 class RenderParams:
     """raytrace.zig:102-108 plus the knobs of the GPU path."""

@@ -136,6 +136,7 @@ SIGNATURES = [
     ("zrt_last_error", C.c_char_p, []),
     ("zrt_abi_version", C.c_int, []),
     ("zrt_build_info", C.c_char_p, []),
+    ("zrt_build_id", C.c_char_p, []),
     ("zrt_ctx_create", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(_P)]),
     ("zrt_ctx_destroy", C.c_int, [_P]),
     ("zrt_ctx_tile_count", C.c_int, [_P, C.POINTER(Params), C.POINTER(C.c_uint32)]),

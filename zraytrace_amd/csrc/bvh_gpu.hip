@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -246,6 +247,9 @@ bool build_bvh_device(const zrt_prim* prims, uint32_t n, int device, BuiltBvh* o
     hi4[i] = make_float4(b.mx[0], b.mx[1], b.mx[2], 0.0f);
   }
   BVHCHK(hipSetDevice(device));
+  // tests: a HIP failure inside the device build (flatten_scene must fall back to the host build)
+  if (const char* e = std::getenv("ZRT_DEBUG_BVH_DEVICE_FAIL"))
+    if (std::atoi(e) != 0) BVHCHK(hipErrorOutOfMemory);
   hipStream_t st = nullptr;
   BVHCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   struct StreamGuard {

@@ -1521,6 +1521,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       if (__ballot(active) != 0ull) {
         gate = min(gate + a.sync, unit_end);
       } else {
+        if (cur_lt != 0xffffffffu)  // the finished unit's chunk sums, [chunk][pixel slot]: one 1 KiB store per wave
+          a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
         if (a.unit_cost && cur_lt != 0xffffffffu && lane == 0) a.unit_cost[cur_lt] = iters;
         if (a.scanlines && cur_lt != 0xffffffffu) {  // the finished unit's counters, per frame row
           flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
@@ -1641,10 +1643,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       acc_g += col.y;
       acc_b += col.z;
       in_sample = false;
-      if (++sample == unit_end) {  // chunk done: its sequential sum; partial is [chunk][pixel slot]
-        a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
-        active = false;
-      }
+      if (++sample == unit_end) active = false;  // chunk done: its sequential sum, stored when the unit ends
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
   }
@@ -1776,6 +1775,11 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     }
     // ---- refill: the wave's unit is done (lanes wait at unit ends only)
     if (__ballot(active) == 0ull) {
+      // the finished unit's chunk sums, [chunk][pixel slot], all 64 lanes at once: one
+      // 1 KiB store per wave (stored by each lane as it finished, the lines went out
+      // to memory in 32-B pieces: twice the bytes, profiles/r03 write budget)
+      if (cur_lt != 0xffffffffu)
+        a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
       if (a.scanlines && cur_lt != 0xffffffffu) {
         flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
         c_depth = c_refl = c_bg = 0;
@@ -1834,8 +1838,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       acc_g += col.y;
       acc_b += col.z;
       in_sample = false;
-      if (++sample == unit_end) {  // chunk done: its sequential sum
-        a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
+      if (++sample == unit_end) {  // chunk done: its sequential sum (stored at the unit's end)
         active = false;
         continue;
       }
@@ -2348,7 +2351,19 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   uint32_t depth = 0;
   if (use_bvh) {
     BuiltBvh bvh;
-    if (!(device >= 0 && device_bvh(n) && build_bvh_device(s->prims, n, device, &bvh))) bvh = build_bvh(s->prims, n);
+    bool built = false;
+    if (device >= 0 && device_bvh(n)) {
+      // the same tree on the GPU; any HIP failure there (hipMalloc on a busy GPU,
+      // a hipcub error) falls back to the host build, which gives the same tree
+      try {
+        built = build_bvh_device(s->prims, n, device, &bvh);
+      } catch (const Error& e) {
+        if (std::getenv("ZRT_DEBUG_LAUNCH"))
+          std::fprintf(stderr, "zrt preprocess: device BVH build failed (%s); host build\n", e.what());
+        (void)hipGetLastError();  // clear a sticky runtime error of the failed build
+      }
+    }
+    if (!built) bvh = build_bvh(s->prims, n);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: reference BVH %zu nodes in %.1f ms\n", bvh.nodes.size(), now_ms() - t0);
     depth = bvh.max_depth;

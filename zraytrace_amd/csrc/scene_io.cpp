@@ -622,6 +622,19 @@ int zrt_scene_read(const char* path, zrt_scene_data** out, zrt_camera* camera) {
     zrt::FlatScene& fs = h->sd->flat;
     zrt_camera cam;
     get(in.f, &cam, sizeof(cam));
+    // the header's counts come from the file: check that their arrays (and, as
+    // each is read, every image) fit in what remains of it before allocating, so
+    // a corrupt or foreign file fails with ZRT_E_PARSE instead of asking for up
+    // to 2^32 records
+    const long here = std::ftell(in.f);
+    if (here < 0 || std::fseek(in.f, 0, SEEK_END) != 0) throw zrt::Error(ZRT_E_IO, "cannot seek in scene file");
+    const long end = std::ftell(in.f);
+    if (end < here || std::fseek(in.f, here, SEEK_SET) != 0) throw zrt::Error(ZRT_E_IO, "cannot seek in scene file");
+    uint64_t left = uint64_t(end - here);
+    const uint64_t arrays = sizeof(zrt_prim) * uint64_t(head[4]) + sizeof(zrt_material) * uint64_t(head[5]) +
+                            sizeof(zrt_texture) * uint64_t(head[6]) + 2 * sizeof(uint32_t) * uint64_t(head[7]);
+    if (arrays > left) return zrt::fail(ZRT_E_PARSE, std::string(path) + ": header counts exceed the file size");
+    left -= arrays;
     fs.prims.resize(head[4]);
     fs.materials.resize(head[5]);
     fs.textures.resize(head[6]);
@@ -632,6 +645,9 @@ int zrt_scene_read(const char* path, zrt_scene_data** out, zrt_camera* camera) {
       uint32_t wh[2];
       get(in.f, wh, sizeof(wh));
       if (uint64_t(wh[0]) * wh[1] > (1ull << 30)) return zrt::fail(ZRT_E_PARSE, "image too large");
+      const uint64_t bytes = sizeof(float) * 3 * uint64_t(wh[0]) * wh[1];
+      if (bytes > left) return zrt::fail(ZRT_E_PARSE, std::string(path) + ": image exceeds the file size");
+      left -= bytes;
       auto img = zrt::Image::init(wh[0], wh[1]);
       get(in.f, img->pixels.data(), sizeof(float) * img->pixels.size());
       fs.images.push_back(zrt_image{wh[0], wh[1], img->pixels.data()});

@@ -94,6 +94,8 @@ class TileFrame:
             self.gathered = torch.empty(world * max(1, self.max_tiles) * 64 * 3, dtype=torch.float32, device=dev)
             self.frame = torch.empty(params.height * params.width * 3, dtype=torch.float32, device=dev)
         self.p0 = RenderParams(**{**params.__dict__, "rank": 0})
+        self.gather_ms = []  # per step: the gather (+ assemble on rank 0), HIP events on self.stream
+        self._ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
 
     def step(self, params=None) -> float:
         """One frame; returns the render launch's kernel time in ms (HIP events
@@ -104,10 +106,15 @@ class TileFrame:
         with torch.cuda.stream(self.stream):
             self.ctx.render_tiles(self.scene.camera, p, self.tiles.data_ptr(), self.stream.cuda_stream)
             kms = self.ctx.kernel_ms()
+            self._ev[0].record(self.stream)
             g = gather_tiles(self.tiles, self.counts, self.rank, self.world, dst=0, out=self.gathered)
             if self.rank == 0:
                 self.ctx.assemble_padded(self.p0, g.data_ptr(), max(1, self.max_tiles), self.frame.data_ptr(),
                                          self.stream.cuda_stream)
+            self._ev[1].record(self.stream)
+        if params is None:
+            self._ev[1].synchronize()
+            self.gather_ms.append(self._ev[0].elapsed_time(self._ev[1]))
         return kms
 
     def image(self):
