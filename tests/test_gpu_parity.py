@@ -651,3 +651,54 @@ def test_trace_grazing_rays_bit_exact(scenes, which):
     for trav in TRAVERSALS:
         t, p = z.trace(keep, z.RenderParams(1, 1, 1, 1, traversal=trav), o, d)
         assert_same_hits(t, p, t_ref, p_ref)
+
+
+# ---- adversarial cases against FAST's exactness argument ----
+
+def _trace_all(scene, o, d, keep=None):
+    t_ref, p_ref = O.trace(scene, True, o, d)
+    bad = {}
+    for trav in TRAVERSALS:
+        t, p = z.trace(keep or scene, z.RenderParams(1, 1, 1, 1, traversal=trav), o, d)
+        wrong = (p != p_ref) | ~same_bits(t, t_ref)
+        if wrong.any():
+            bad[trav] = int(wrong.sum())
+    return p_ref, bad
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_trace_near_miss_spheres_bit_exact(seed):
+    """Rays just outside small, distant spheres (tests/adversarial_rays.py): the
+    rounded disc of sphere.zig:31-41 accepts thousands of them although they miss
+    the sphere (and its box), and some run past facing triangles placed just in
+    front of tangent points.  Every traversal returns the oracle's answer."""
+    import adversarial_rays as A
+    scene, o, d = A.near_miss_scene(seed)
+    p_ref, bad = _trace_all(scene, o, d)
+    assert (p_ref >= 0).sum() > 10000
+    assert not bad, f"rays differing from the oracle, per traversal: {bad}"
+
+
+@pytest.mark.parametrize("which,scale,translate", [(2, 1.0, 1e3), (2, 1.0, 1e4), (2, 1e-3, 0.0), (2, 1e3, 0.0),
+                                                   (3, 1.0, 1e3), (3, 1.0, 1e4), (3, 1e-3, 0.0), (3, 1e3, 0.0)])
+def test_trace_transformed_scenes_bit_exact(scenes, which, scale, translate):
+    """the bunny and teapot scenes (ground sphere included)
+    translated by 10^3 / 10^4 and scaled by 10^-3 / 10^3, with the grazing rays of
+    tests/grazing_rays.py and random rays: every traversal equals the oracle."""
+    import adversarial_rays as A
+    pr = A.prim_array(scenes(which).view.contents)
+    scene, o, d = A.transformed_case(O, pr, scale, translate, seed=which)
+    p_ref, bad = _trace_all(scene, o, d)
+    assert (p_ref >= 0).mean() > 0.2
+    assert not bad, f"rays differing from the oracle, per traversal: {bad}"
+
+
+@pytest.mark.parametrize("translate", [1e3, 1e4])
+def test_trace_far_spheres_bit_exact(translate):
+    """bvh.zig:262-291's spheres and rays moved 10^3 / 10^4 from the origin, plus
+    grazing rays: every traversal equals the oracle."""
+    import adversarial_rays as A
+    scene, o, d = A.far_spheres_case(O, translate)
+    p_ref, bad = _trace_all(scene, o, d)
+    assert (p_ref >= 0).sum() > 300
+    assert not bad, f"rays differing from the oracle, per traversal: {bad}"

@@ -209,3 +209,40 @@ def test_grazing_rays_run_in_box_planes(scenes):
     assert (p >= 0).mean() > 0.5
     assert (d == 0).any(axis=1).mean() > 0.35
     assert (p != pl).sum() > 10
+
+
+def test_near_miss_sphere_rays_are_accepted_outside():
+    """tests/adversarial_rays.py pins its point: the reference's own sphere test
+    (sphere.zig:31-41, restated by the oracle) accepts thousands of rays whose
+    exact line misses the sphere - most of them outside the sphere's box too -
+    so a traversal that culls boxes a ray does not cross must allow for it
+    (DESIGN.md §3 "Spheres")."""
+    import ctypes as C
+    import adversarial_rays as A
+    scene, o, d = A.near_miss_scene(0)
+    _, p = O.trace(C.pointer(scene), True, o, d)
+    pr = A.prim_array(scene)
+    dd = A._unit(d.astype(np.float64))
+    hit = np.nonzero(p >= 0)[0]
+    hit = hit[pr["kind"][p[hit]] == 0]
+    c = pr["center"][p[hit]].astype(np.float64)
+    r = pr["radius"][p[hit]].astype(np.float64)
+    oc = o[hit].astype(np.float64) - c
+    hb = (oc * dd[hit]).sum(1)
+    dist = np.sqrt(np.maximum((oc * oc).sum(1) - hb * hb, 0.0))
+    out = dist > r
+    # the exact line misses the box: outside the slab of the face the ray runs along
+    q = o[hit].astype(np.float64) + dd[hit] * hb[:, None] * -1.0  # closest approach to the center
+    box_miss = (np.abs(q - c) > r[:, None]).any(1)
+    assert out.sum() > 3000 and (out & box_miss).sum() > 1000, (int(out.sum()), int((out & box_miss).sum()))
+
+
+def test_transformed_prims_are_the_stated_map(scenes):
+    """adversarial_rays.transformed_prims: v -> v * s + t per coordinate in f32."""
+    import adversarial_rays as A
+    pr = A.prim_array(scenes(2).view.contents)
+    sph, tri = A.transformed_prims(pr, 1e3, 1e4)
+    t = pr[pr["kind"] == 1][0]
+    exp = (t["a"].astype(np.float32) * np.float32(1e3) + np.float32(1e4)).astype(np.float32)
+    assert np.array_equal(np.asarray(tri[0][0], np.float32), exp)
+    assert sph[0][1] == float(np.float32(pr[pr["kind"] == 0][0]["radius"]) * np.float32(1e3))

@@ -4,6 +4,8 @@
 #   pmc:<cfg>   rocprofv3 --pmc passes of config <cfg> (tools/gpu_pmc.sh)
 #   bench:<cfg> one bench line of config <cfg>
 #   rehearse    the N-rank path on one GPU over gloo (tools/gpu_rehearse_dist.sh)
+#   adv         the adversarial exactness tests alone, reported without stopping the session
+# PYTEST_K: a -k expression for the main test run (e.g. "not near_miss")
 # <cfg>: c2 | c3 | c4 | c5 (BASELINE.json configs)
 # usage: bash tools/gpu_session.sh <tag> [--no-tests] [step...]
 set -o pipefail
@@ -19,7 +21,7 @@ cfg_args() {
   esac
 }
 if [ "$1" == "--no-tests" ]; then shift; else
-  (cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1); rc=$?
+  (cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/tests.log 2>&1); rc=$?
   tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 (cd $R && timeout -k 10 600 python bench.py > $O/c4.json 2> $O/c4.err) || { echo "bench failed"; tail -5 $O/c4.err; exit 1; }
@@ -31,6 +33,8 @@ for step in "$@"; do
     bench) (cd $R && timeout -k 10 900 python bench.py $(cfg_args $c) > $O/$c.json 2> $O/$c.err) || { echo "bench $c failed"; tail -5 $O/$c.err; exit 1; }
            python -c "import json; d=json.load(open('$O/$c.json')); print('$c', d['value'], d['ms_per_step'], d['frame_sha1'][:12])" ;;
     rehearse) bash $R/tools/gpu_rehearse_dist.sh $TAG/dist || exit 1 ;;
+    adv) (cd $R && timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 300 --timeout-method thread -k "near_miss or transformed or far_spheres" > $O/adv.log 2>&1); rc=$?
+         tail -15 $O/adv.log; [ $rc -le 1 ] || exit $rc ;;
   esac
 done
 echo session-done

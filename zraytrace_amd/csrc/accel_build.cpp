@@ -33,7 +33,10 @@
 //   its box by a few ulps of the coordinates, and growing the box in space grows
 //   each axis's t interval by that distance x |1/d_k| - the right slack for a
 //   ray (nearly) parallel to a box face, at no cost per node (DESIGN.md §3
-//   "Grazing rays").
+//   "Grazing rays").  An inner child whose subtree holds a sphere is grown by
+//   `sphere_grow` more: the rounded sphere test accepts rays that pass outside
+//   the sphere by up to ~sqrt(u) |oc| and errs by as much in t (DESIGN.md §3
+//   "Spheres").  A leaf child holding a sphere stores ref a - kSphereSlotBias.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -71,12 +74,14 @@ struct Item {
   Aabb box;
   float c[3];
   int32_t leaf;
+  bool sphere;
 };
 
 struct Node2 {
   Aabb box;
   int32_t left = -1, right = -1;  // children (Node2 indices); -1 for a leaf
   int32_t leaf = -1;              // reference leaf index for a leaf
+  bool sphere = false;            // the subtree holds a sphere
 };
 
 struct Builder2 {
@@ -95,6 +100,7 @@ struct Builder2 {
     const size_t n = hi - lo;
     if (n == 1) {
       nodes[me].leaf = items[lo].leaf;
+      nodes[me].sphere = items[lo].sphere;
       return me;
     }
     // binned SAH over centroids
@@ -155,6 +161,7 @@ struct Builder2 {
     const int32_t r = build(mid, hi);
     nodes[me].left = l;
     nodes[me].right = r;
+    nodes[me].sphere = nodes[size_t(l)].sphere || nodes[size_t(r)].sphere;
     return me;
   }
 };
@@ -163,7 +170,7 @@ void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
 
 }  // namespace
 
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate) {
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate, float sphere_grow) {
   WideBvh out;
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
@@ -176,6 +183,7 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
       items[i].c[k] = 0.5f * (L.mn[k] + L.mx[k]);
     }
     items[i].leaf = int32_t(i);
+    items[i].sphere = ref_is_sphere(L.prim_a) || ref_is_sphere(L.prim_b);
   }
   if (n == 0) return out;
   Builder2 b{items, {}};
@@ -282,12 +290,13 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
         if (N[c].leaf >= 0) {
           ref = leaves[size_t(N[c].leaf)].prim_a;
           ref_b = leaves[size_t(N[c].leaf)].prim_b;
+          if (N[c].sphere) ref -= kSphereSlotBias;
         } else {
           ref = pos[size_t(wide_of[c])];
           ref_b = 0;
           double cmax = 0.0;
           for (int a = 0; a < 3; ++a) cmax = std::max({cmax, std::fabs(double(box.mn[a])), std::fabs(double(box.mx[a]))});
-          const double g = double(inflate) * cmax;
+          const double g = double(inflate) * cmax + (N[c].sphere ? double(sphere_grow) : 0.0);
           for (int a = 0; a < 3 && g > 0.0; ++a) {  // grown outward, rounded outward
             float lo = float(double(box.mn[a]) - g), hi = float(double(box.mx[a]) + g);
             if (double(lo) > double(box.mn[a]) - g) lo = std::nextafter(lo, -INFINITY);

@@ -22,10 +22,22 @@ struct WideBvh {
   uint32_t n_top = 0;           // nodes of the top levels, stored first (0 .. n_top-1)
 };
 
+// A leaf slot holding a sphere stores its ref a minus kSphereSlotBias (below
+// -2^30, where no other ref lies): render.hip opens such slots with the
+// reference's loose test against t_max = +inf (DESIGN.md §3 "Spheres") and adds
+// the bias back before testing the primitives.
+constexpr int32_t kSphereSlotBias = int32_t(1) << 30;
+
 // top_levels: how many levels (root = 1) are stored first, breadth-first.
 // inflate: inner children's boxes are stored grown on every side by this much
 // times their own largest |coordinate| (rounded outward); leaf children keep
 // the reference leaf's box bit for bit.
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels = 2, float inflate = 0.0f);
+// sphere_grow: inner children whose subtree holds a sphere are grown by this
+// much more (absolute): the rounded sphere test's reach beyond the sphere.
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels = 2, float inflate = 0.0f,
+                       float sphere_grow = 0.0f);
+
+// primitive-slot ref of render.hip, -(2*slot + kind) - 1: kind 0 is a sphere
+inline bool ref_is_sphere(int32_t ref) { return ref < 0 && ((-(int64_t(ref) + 1)) & 1) == 0; }
 
 }  // namespace zrt

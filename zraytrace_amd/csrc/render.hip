@@ -108,6 +108,12 @@ struct KArgs {
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
   float scene_extent;     // the triangles' largest |coordinate| (ray_slack)
+  // Spheres (DESIGN.md §3 "Spheres"): the reference BVH nodes whose subtree holds
+  // a sphere (1 byte each), and the origins the wide tree's sphere growth was
+  // sized for: max_k |o_k - root_c[k]| <= origin_bound (other rays are traced the
+  // reference's way, ray_origin_ok)
+  const uint8_t* __restrict__ ref_sph;
+  float root_c[3], origin_bound;
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -377,7 +383,7 @@ __device__ __forceinline__ float ray_slack(float extent, float m) {
 // margin) and reports the entry distance for near-first ordering.
 template <bool FAST>
 __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const RayT& r, float t_max,
-                                         float* entry, float slack = 0.0f) {
+                                         float* entry, float slack = 0.0f, bool narrow = true) {
   const float t_min = 0.001f;
   float a0 = (lo.x - r.ox) * r.ix, a1 = (hi.x - r.ox) * r.ix;
   float b0 = (lo.y - r.oy) * r.iy, b1 = (hi.y - r.oy) * r.iy;
@@ -396,7 +402,7 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && !(en > __builtin_fmaf(ex, ray_rel(ray_m(r)), slack));
+    ok = ok && (!narrow || !(en > __builtin_fmaf(ex, ray_rel(ray_m(r)), slack)));
     *entry = en;
   }
   return ok;
@@ -629,9 +635,25 @@ struct ExcessAcc {
 #else
 #define ZRT_REPLAY_ATTR __noinline__
 #endif
+// A ray whose origin lies where the wide tree's sphere growth was sized for
+// (KArgs::origin_bound, DESIGN.md §3 "Spheres"); other rays (none in a render of
+// the reference's scenes: their cameras lie inside that region) are traced the
+// reference's way alone.
+__device__ __forceinline__ bool ray_origin_ok(const KArgs& a, const RayT& r) {
+  const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox - a.root_c[0]), __builtin_fabsf(r.oy - a.root_c[1])),
+                                  __builtin_fabsf(r.oz - a.root_c[2]));
+  return m <= a.origin_bound;
+}
+
+// The reference's traversal (bvh.zig:187-205) for a ray FAST flagged: left-first
+// over the reference BVH, every box through the reference's loose test against the
+// current best, so every leaf is accepted or rejected as the reference does.
+// narrow: also cull boxes the ray does not cross (the narrowed test with the
+// grazing slack) - except boxes holding a sphere, whose rounded
+// test reaches beyond the sphere (KArgs::ref_sph); false: the reference's test alone.
 template <class StackT>
 __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, StackT* __restrict__ stk, uint32_t gl,
-                                              float& best_t, int& best) {
+                                              float& best_t, int& best, bool narrow = true) {
   const uint32_t rows = a.lds_rows, cap = a.ref_stack;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float slack = ray_slack(a.scene_extent, ray_m(r));
@@ -649,7 +671,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
     // emptiness test (a box the ray does not cross holds no hit):
     // left-first with the reference's t_max, so every leaf is accepted or
     // rejected exactly as the reference does it, in ~1 % of its node visits
-    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e, slack)) continue;
+    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e, slack, narrow && a.ref_sph[idx] == 0)) continue;
     const int left = as_int(lo.w), right = as_int(hi.w);
     if (left < 0) {
       prim_test<false, false>(a.prims, left, r, best_t, best, c_tri, c_sph);
@@ -669,6 +691,16 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
 }
 
 
+// BINARY's node test: the narrowed test with the grazing slack against tb, or,
+// for a node whose subtree holds a sphere (KArgs::ref_sph), the reference's loose
+// test against t_max = +inf: the rounded sphere test reaches beyond the sphere
+// and its box by ~sqrt(u) |oc| and errs by as much in t (DESIGN.md §3 "Spheres").
+__device__ __forceinline__ bool binary_test(const KArgs& a, int idx, const float4 lo, const float4 hi, const RayT& r,
+                                            float tb, float* e, float slack) {
+  if (a.ref_sph[idx]) return box_test<true>(lo, hi, r, __builtin_inff(), e, 0.0f, false);
+  return box_test<true>(lo, hi, r, tb, e, slack);
+}
+
 // Closest hit over the BVH.  FAST: near-first order with the narrowed slab
 // test; REFERENCE: left-first DFS with exactly bvh.zig:187-205's tests.
 template <bool FAST, bool STATS, class StackT>
@@ -683,7 +715,10 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
-    if (!box_test<true>(lo, hi, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) return;
+    if (!binary_test(a, 0, lo, hi, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
+      if (!ray_origin_ok(a, r)) reference_replay<StackT>(a, r, stk, 0u, best_t, best, false);
+      return;
+    }
     int left = as_int(lo.w), right = as_int(hi.w);
     for (;;) {
       if (left < 0) {
@@ -695,8 +730,8 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         if (STATS) c_nodes += 2;
         const float tb = __builtin_fabsf(best_t) * kOpen + slack;
         float el, er;
-        const bool hl = box_test<true>(l0, l1, r, tb, &el, slack);
-        const bool hr = box_test<true>(r0, r1, r, tb, &er, slack);
+        const bool hl = binary_test(a, left, l0, l1, r, tb, &el, slack);
+        const bool hr = binary_test(a, right, r0, r1, r, tb, &er, slack);
         if (hl && hr) {
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
@@ -716,7 +751,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const int idx = stk[sp * stride];
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
-        if (box_test<true>(p0, p1, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
+        if (binary_test(a, idx, p0, p1, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
           found = true;
@@ -728,6 +763,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
     // the order hazard of DESIGN.md §3, as in traverse_wide (the stack is all in LDS here)
     if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<true>(a, r, best_t, best), 0))
       reference_replay<StackT>(a, r, stk, 0u, best_t, best);
+    if (__builtin_expect(!ray_origin_ok(a, r), 0)) reference_replay<StackT>(a, r, stk, 0u, best_t, best, false);
   } else {
     stk[0] = 0;
     sp = 1;
@@ -814,6 +850,19 @@ __device__ __forceinline__ SlotT slot_interval(float nx, float ny, float nz, flo
   s.ex = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tb));
   return s;
 }
+#ifndef ZRT_SPHERE_SLOTS
+#define ZRT_SPHERE_SLOTS 1  // A/B only: 0 culls sphere leaves like triangle leaves (not exact, DESIGN.md §3 "Spheres")
+#endif
+// The reference's loose test (aabb.zig:109-127) with t_max = +inf: every axis's
+// (post-swap) slab [n, f] reaches past t_min and is not empty.  max(n, t_min) /
+// min(f, +inf) as maxNum / minNum: a NaN bound constrains nothing, as math.max /
+// math.min with t_min / t_max leave it in the reference.
+__device__ __forceinline__ bool static_ok(float nx, float ny, float nz, float fx, float fy, float fz) {
+  const float t_min = 0.001f, inf = __builtin_inff();
+  return (__builtin_fminf(fx, inf) > __builtin_fmaxf(nx, t_min)) && (__builtin_fminf(fy, inf) > __builtin_fmaxf(ny, t_min)) &&
+         (__builtin_fminf(fz, inf) > __builtin_fmaxf(nz, t_min));
+}
+
 // The reference's own loose test (aabb.zig:109-127) of leaf slot k whose
 // narrowed test passed with en >= ex (rare; with en < ex it passes outright:
 // an <= en < ex <= ax on every axis): each axis on its own, its distances
@@ -853,6 +902,22 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
   const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
   return loose && !(en > ex * ray_rel(ray_m(r)));
+}
+
+// static_ok of leaf slot k, its slab distances recomputed from the node in memory
+// (the same two roundings as wide_iter's) so that none stays live across the node
+__device__ __forceinline__ bool static_ok_slot(const float4* __restrict__ q, int k, const RayT& r, bool sx, bool sy,
+                                               bool sz) {
+  const float* f = reinterpret_cast<const float*>(q) + k;
+#if ZRT_OCT_COPIES
+  (void)sx; (void)sy; (void)sz;
+  const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
+#else
+  const int px = sx ? 12 : 0, py = sy ? 16 : 4, pz = sz ? 20 : 8;
+  const int qx = sx ? 0 : 12, qy = sy ? 4 : 16, qz = sz ? 8 : 20;
+#endif
+  return static_ok((f[px] - r.ox) * r.ix, (f[py] - r.oy) * r.iy, (f[pz] - r.oz) * r.iz, (f[qx] - r.ox) * r.ix,
+                   (f[qy] - r.oy) * r.iy, (f[qz] - r.oz) * r.iz);
 }
 
 constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
@@ -1018,6 +1083,21 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
     if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
   }
+#if ZRT_SPHERE_SLOTS
+  // leaf slots holding a sphere (ref a - 2^30, accel_build.hpp): opened when the
+  // reference's loose test passes against t_max = +inf.  The rounded sphere test
+  // accepts rays that pass outside the sphere - and its box - by up to ~sqrt(u)|oc|
+  // and errs by as much in t (DESIGN.md §3 "Spheres"), so neither the narrowed
+  // test nor the current best may cull them; every sphere hit of a static-ok
+  // leaf is then seen, and the order-hazard tests see it too.  (A wave-uniform
+  // branch: nodes with sphere leaves are few.)
+  if (__builtin_expect(__ballot(min(min(r0, r1), min(r2, r3)) < -kSphereSlotBias) != 0ull, 0)) {
+    if (r0 < -kSphereSlotBias) { o0 = static_ok_slot(q, 0, r, sx, sy, sz); r0 += kSphereSlotBias; }
+    if (r1 < -kSphereSlotBias) { o1 = static_ok_slot(q, 1, r, sx, sy, sz); r1 += kSphereSlotBias; }
+    if (r2 < -kSphereSlotBias) { o2 = static_ok_slot(q, 2, r, sx, sy, sz); r2 += kSphereSlotBias; }
+    if (r3 < -kSphereSlotBias) { o3 = static_ok_slot(q, 3, r, sx, sy, sz); r3 += kSphereSlotBias; }
+  }
+#endif
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
   const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
   int32_t next = -1;
@@ -1175,6 +1255,11 @@ __device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, Stack
 #else
     reference_replay<StackT>(a, r, stk, gl, best_t, best);
 #endif
+  }
+  // an origin farther out than the sphere growth was sized for: the reference's way alone
+  if (__builtin_expect(!ray_origin_ok(a, r), 0)) {
+    if (STATS) ++c_replays;
+    reference_replay<StackT>(a, r, stk, gl, best_t, best, false);
   }
 }
 
@@ -2271,6 +2356,8 @@ struct zrt_ctx {
   zrt::DevBuf<float> texels, lut255;
   zrt::DevBuf<uint32_t> texels8;
   zrt::DevBuf<uint32_t> leaf_of_slot;
+  zrt::DevBuf<uint8_t> ref_sph;
+  float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
@@ -2323,6 +2410,8 @@ struct HostScene {
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;  // KArgs::tri_rcp_fast
   float scene_extent = 0.0f;  // KArgs::scene_extent
+  float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;  // KArgs::root_c / origin_bound
+  std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
   std::vector<float> tex, lut;
@@ -2408,8 +2497,37 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       nodes[2 * i + 1] = hi;
     }
     c->n_nodes = uint32_t(bvh.nodes.size());
+    // Spheres (DESIGN.md §3 "Spheres").  The rounded disc of sphere.zig:31-41 errs by
+    // E <= 32 u (|oc|^2 + r^2) (u = 2^-24, three rounded dot products and two
+    // subtractions), so an accepted ray passes within sqrt(r^2 + E) - r <= sqrt(E) of
+    // the sphere and its hit errs by <= 1.5 sqrt(E) in t: subtrees holding a sphere
+    // are grown by 2 sqrt(E) = 2^-8.5 R, R >= |oc| + r for every ray whose origin
+    // lies within 2 H of the root box's center on every axis (H: its largest half
+    // extent; |oc| <= 2 sqrt(3) H + sqrt(3) H, r <= H).  Rays from farther out are
+    // traced the reference's way (render.hip ray_origin_ok).
+    c->ref_sph.assign(bvh.nodes.size(), 0);
+    bool any_sphere = false;
+    for (size_t i = bvh.nodes.size(); i-- > 0;) {  // pre-order: children after their parent
+      const BuildNode& b = bvh.nodes[i];
+      uint8_t f = 0;
+      for (const int32_t ch : {b.left, b.right}) {
+        if (ch >= 0) f |= c->ref_sph[size_t(ch)];
+        else f |= s->prims[uint32_t(-ch - 1)].kind == ZRT_PRIM_SPHERE ? 1 : 0;
+      }
+      c->ref_sph[i] = f;
+      any_sphere = any_sphere || f;
+    }
+    float H = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      const BuildNode& root = bvh.nodes[0];
+      c->root_c[k] = 0.5f * root.mn[k] + 0.5f * root.mx[k];
+      H = std::max(H, 0.5f * (root.mx[k] - root.mn[k]));
+    }
+    if (!(H < 0x1p100f)) H = 0x1p100f;  // NaN / huge extents: every origin fails ray_origin_ok's bound
+    c->origin_bound = 2.0f * H;
+    const float sphere_grow = any_sphere ? float(std::ldexp(std::sqrt(2.0), -9) * (3.0 * std::sqrt(3.0) + 1.0) * double(H)) : 0.0f;
     const double tw = now_ms();
-    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f);
+    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
@@ -2563,6 +2681,9 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->texels8.upload(h.tex8);
   c->lut255.upload(h.lut);
   c->leaf_of_slot.upload(h.leaf_of_slot);
+  c->ref_sph.upload(h.ref_sph);
+  for (int k = 0; k < 3; ++k) c->root_c[k] = h.root_c[k];
+  c->origin_bound = h.origin_bound;
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -3040,6 +3161,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.stack_depth = stack_depth;
     a.ref_stack = std::min(c->stack_depth, stack_depth);
     a.leaf_of_slot = c->leaf_of_slot.p;
+    a.ref_sph = c->ref_sph.p;
+    for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
+    a.origin_bound = c->origin_bound;
     a.wnodes = c->wnodes.p;
     a.wide_stride = c->wide_stride;
     a.lds_rows = lds_rows;
@@ -3591,6 +3715,9 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.stack_depth = stack_depth;
     a.ref_stack = c->stack_depth;
     a.leaf_of_slot = c->leaf_of_slot.p;
+    a.ref_sph = c->ref_sph.p;
+    for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
+    a.origin_bound = c->origin_bound;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
