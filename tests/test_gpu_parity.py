@@ -136,13 +136,21 @@ def test_render_bit_exact_vs_oracle(scenes, case, traversal):
         assert gs["node_visits"] == rs["node_visits"]
 
 
-@pytest.mark.parametrize("loop", ["lockstep", "wavefront"])
+def set_loop(monkeypatch, loop):
+    """Force one FAST sampling loop: lockstep (render_loop), wavefront
+    (render_loop_wf) or path pool (render_loop_pool)."""
+    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    monkeypatch.setenv("ZRT_POOL", "1" if loop == "pool" else "0")
+
+
+@pytest.mark.parametrize("loop", ["lockstep", "wavefront", "pool"])
 @pytest.mark.parametrize("case", [c for c in CASES if c[0] != 1], ids=[f"scene{c[0]}" for c in CASES if c[0] != 1])
 def test_render_loops_bit_exact(scenes, case, loop, monkeypatch):
-    """Both FAST sampling loops (render_loop and the wavefront render_loop_wf,
-    DESIGN.md §3) on every BVH scene, with more samples per pixel and a chunk that
-    splits them: images, counters and per-scanline counters equal the oracle's."""
-    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    """The three FAST sampling loops (render_loop, the wavefront render_loop_wf and
+    the path-pool render_loop_pool) on every BVH scene, with more
+    samples per pixel and a chunk that splits them: images, counters and
+    per-scanline counters equal the oracle's."""
+    set_loop(monkeypatch, loop)
     idx, w, h, _, depth = case
     s = scenes(idx)
     p = z.RenderParams(w, h, 24, depth, sample_chunk=7)
@@ -171,7 +179,8 @@ def test_c5_substitute_bit_exact(scenes):
             assert gs[k] == rs[k], k
 
 
-@pytest.mark.parametrize("loop,rows", [("wavefront", None), ("wavefront", "2"), ("lockstep", "2")])
+@pytest.mark.parametrize("loop,rows", [("wavefront", None), ("wavefront", "2"), ("lockstep", "2"), ("pool", None),
+                                       ("pool", "2")])
 def test_c5_substitute_depth20_vs_golden(scenes, loop, rows, monkeypatch):
     """the C5 path at its real depth.  Scene 6 at 32x32 x 2 spp,
     max depth 20, 1-sample chunks, against the oracle's frame, progress counters
@@ -186,7 +195,7 @@ def test_c5_substitute_depth20_vs_golden(scenes, loop, rows, monkeypatch):
     import torch
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_depth20.npz"))
     w, h, spp, depth, chunk = (int(x) for x in g["params"])
-    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    set_loop(monkeypatch, loop)
     monkeypatch.setenv("ZRT_ATT_LDS_ROWS", "0")
     if rows:
         monkeypatch.setenv("ZRT_STACK_LDS_ROWS", rows)

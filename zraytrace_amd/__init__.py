@@ -41,7 +41,10 @@ _ID_SRC = ("render.hip", "bvh_gpu.hip", "accel_build.cpp", "accel_build.hpp", "b
 def build_id() -> str:
     """zrt_build_id() of the loaded library: sha1 of the kernel sources (16 hex)
     - sha1 of the device compile flags (8)."""
-    return lib().zrt_build_id().decode()
+    L = lib()
+    if not hasattr(L, "zrt_build_id"):  # an A/B variant built from older sources (ZRT_LIB)
+        return "unknown"
+    return L.zrt_build_id().decode()
 
 
 def build_id_of_sources() -> str:

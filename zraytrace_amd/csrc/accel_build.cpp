@@ -170,7 +170,8 @@ void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
 
 }  // namespace
 
-WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate, float sphere_grow) {
+WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate, float sphere_grow,
+                       bool mark_spheres) {
   WideBvh out;
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
@@ -290,7 +291,7 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
         if (N[c].leaf >= 0) {
           ref = leaves[size_t(N[c].leaf)].prim_a;
           ref_b = leaves[size_t(N[c].leaf)].prim_b;
-          if (N[c].sphere) ref -= kSphereSlotBias;
+          if (N[c].sphere && mark_spheres) ref -= kSphereSlotBias;
         } else {
           ref = pos[size_t(wide_of[c])];
           ref_b = 0;

@@ -34,8 +34,10 @@ constexpr int32_t kSphereSlotBias = int32_t(1) << 30;
 // the reference leaf's box bit for bit.
 // sphere_grow: inner children whose subtree holds a sphere are grown by this
 // much more (absolute): the rounded sphere test's reach beyond the sphere.
+// mark_spheres: leaf slots holding a sphere carry ref a - kSphereSlotBias (the
+// kernel must then be built to decode them: render.hip ZRT_SPHERE_SLOTS).
 WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels = 2, float inflate = 0.0f,
-                       float sphere_grow = 0.0f);
+                       float sphere_grow = 0.0f, bool mark_spheres = false);
 
 // primitive-slot ref of render.hip, -(2*slot + kind) - 1: kind 0 is a sphere
 inline bool ref_is_sphere(int32_t ref) { return ref < 0 && ((-(int64_t(ref) + 1)) & 1) == 0; }

@@ -106,6 +106,9 @@ struct KArgs {
   uint32_t lds_mat_off;   // the material table (n_mats DevMaterial), when mats_in_lds
   uint32_t n_mats, mats_in_lds;
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
+                       // (path-pool loop: once the queue is empty and fewer than 64 - this lanes traverse)
+  uint32_t lds_pool_off;  // path-pool loop: rays, hits and queues (kBlockPaths paths per block)
+  uint32_t n_paths;       //   paths of the launch (grid x kBlockPaths): the stride of its global attenuation rows
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
   float scene_extent;     // the triangles' largest |coordinate| (ray_slack)
   // Spheres (DESIGN.md §3 "Spheres"): the reference BVH nodes whose subtree holds
@@ -114,6 +117,8 @@ struct KArgs {
   // reference's way, ray_origin_ok)
   const uint8_t* __restrict__ ref_sph;
   float root_c[3], origin_bound;
+  uint32_t check_origins;  // 0: every ray of the launch starts inside the bound (the camera does, checked
+                           // on the host, and scattered rays start at hits), so ray_origin_ok is skipped
 };
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
@@ -640,6 +645,7 @@ struct ExcessAcc {
 // the reference's scenes: their cameras lie inside that region) are traced the
 // reference's way alone.
 __device__ __forceinline__ bool ray_origin_ok(const KArgs& a, const RayT& r) {
+  if (!a.check_origins) return true;  // (wave-uniform: a scalar branch)
   const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox - a.root_c[0]), __builtin_fabsf(r.oy - a.root_c[1])),
                                   __builtin_fabsf(r.oz - a.root_c[2]));
   return m <= a.origin_bound;
@@ -906,9 +912,8 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
 
 // static_ok of leaf slot k, its slab distances recomputed from the node in memory
 // (the same two roundings as wide_iter's) so that none stays live across the node
-__device__ __forceinline__ bool static_ok_slot(const float4* __restrict__ q, int k, const RayT& r, bool sx, bool sy,
-                                               bool sz) {
-  const float* f = reinterpret_cast<const float*>(q) + k;
+template <class FP>
+__device__ __forceinline__ bool static_ok_at(FP f, const RayT& r, bool sx, bool sy, bool sz) {
 #if ZRT_OCT_COPIES
   (void)sx; (void)sy; (void)sz;
   const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
@@ -918,6 +923,18 @@ __device__ __forceinline__ bool static_ok_slot(const float4* __restrict__ q, int
 #endif
   return static_ok((f[px] - r.ox) * r.ix, (f[py] - r.oy) * r.iy, (f[pz] - r.oz) * r.iz, (f[qx] - r.ox) * r.ix,
                    (f[qy] - r.oy) * r.iy, (f[qz] - r.oz) * r.iz);
+}
+// (q is a generic pointer: a node of the top levels lives in LDS - the root,
+// which holds the ground sphere's leaf in every reference scene - and is read
+// with ds_read, not a flat load through the vector memory path)
+__device__ __forceinline__ bool static_ok_slot(const float4* __restrict__ q, int k, const RayT& r, bool sx, bool sy,
+                                               bool sz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__builtin_amdgcn_is_shared(reinterpret_cast<const void*>(q)))
+    return static_ok_at((const __attribute__((address_space(3))) float*)(reinterpret_cast<const float*>(q)) + k, r,
+                        sx, sy, sz);
+#endif
+  return static_ok_at(reinterpret_cast<const float*>(q) + k, r, sx, sy, sz);
 }
 
 constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
@@ -1426,9 +1443,38 @@ constexpr float kInvTwoPi = 1.0f / kTwoPi;
 // (hit_record.zig:28-41) + Material.scatter (material.zig:43-129): absorbed
 // ends the path black, a scatter pushes its attenuation (the product is taken
 // in the recursion's order when the path ends) and moves the ray on.
+// Where a path's attenuation rows live: rows 0 .. a.att_lds_rows-1 in LDS at
+// lds[(3 row + rgb) * lds_stride], the rest in global memory at
+// a.att[(row - a.att_lds_rows) * g_stride + g_index].  The lockstep and wavefront
+// loops index them by lane (stride kBlock / a.n_lanes), the path-pool loop by path.
+struct AttRows {
+  lds_float* __restrict__ lds;
+  uint32_t lds_stride;
+  uint64_t g_index;
+  uint32_t g_stride;
+};
+
+// attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
+// (raytrace.zig:99), over the n rows a path pushed, read back in reverse
+template <bool STATS>
+__device__ __forceinline__ V3 att_product(const KArgs& a, const AttRows& ar, uint32_t n, V3 col, Coh& coh) {
+  for (uint32_t i = n; i-- > 0;) {
+    V3 at;
+    if (i < a.att_lds_rows) {
+      at = mk(ar.lds[(3 * i + 0) * ar.lds_stride], ar.lds[(3 * i + 1) * ar.lds_stride], ar.lds[(3 * i + 2) * ar.lds_stride]);
+    } else {
+      const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
+      if (STATS) ++coh.attr;
+      at = mk(g.x, g.y, g.z);
+    }
+    col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
+  }
+  return col;
+}
+
 template <bool STATS, class R>
 __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __restrict__ mats,
-                                           lds_float* __restrict__ att_l, uint32_t gl, R& rng, int best, float best_t,
+                                           const AttRows& ar, R& rng, int best, float best_t,
                                            V3& o, V3& d, uint32_t& depth_left, bool& path_end, bool& sky, V3& L,
                                            uint32_t& c_bg, uint32_t& c_refl, uint32_t& c_shade, uint32_t& c_tex,
                                            Coh& coh) {
@@ -1533,11 +1579,11 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
         // the first rows live in LDS, deeper ones in global memory
         const uint32_t i = a.max_depth - depth_left;
         if (i < a.att_lds_rows) {
-          att_l[(3 * i + 0) * kBlock] = att.x;
-          att_l[(3 * i + 1) * kBlock] = att.y;
-          att_l[(3 * i + 2) * kBlock] = att.z;
+          ar.lds[(3 * i + 0) * ar.lds_stride] = att.x;
+          ar.lds[(3 * i + 1) * ar.lds_stride] = att.y;
+          ar.lds[(3 * i + 2) * ar.lds_stride] = att.z;
         } else {
-          a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl] = make_float4(att.x, att.y, att.z, 0.0f);
+          a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = make_float4(att.x, att.y, att.z, 0.0f);
           if (STATS) ++coh.attw;
         }
       }
@@ -1701,29 +1747,15 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph, &excess);
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
-      shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
-                        c_shade, c_tex, coh);
+      shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
+                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
     }
 
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
     if (path_end) {
-      // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
-      V3 col = L;
-      if (sky) {
-        // a path that reached the sky traced at depth_left >= 1: all of its
-        // max_depth - depth_left scatters were pushed
-        for (uint32_t i = a.max_depth - depth_left; i-- > 0;) {
-          V3 at;
-          if (i < a.att_lds_rows) {
-            at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
-          } else {
-            const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
-            if (STATS) ++coh.attr;
-            at = mk(g.x, g.y, g.z);
-          }
-          col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
-        }
-      }
+      // a path that reached the sky traced at depth_left >= 1: all of its
+      // max_depth - depth_left scatters were pushed
+      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -1896,29 +1928,15 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
     bool path_end = false, sky = false;
     V3 L = mk(0.0f, 0.0f, 0.0f);
     if (in_sample) {
-      shade_step<STATS>(a, mats, att_l, gl, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl,
-                        c_shade, c_tex, coh);
+      shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
+                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
       if (!path_end && depth_left == 0) {  // the next rayColor is at depth 0: black (raytrace.zig:64-67)
         ++c_depth;
         path_end = true;
       }
     }
     if (path_end) {
-      // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
-      V3 col = L;
-      if (sky) {
-        for (uint32_t i = a.max_depth - depth_left; i-- > 0;) {
-          V3 at;
-          if (i < a.att_lds_rows) {
-            at = mk(att_l[(3 * i + 0) * kBlock], att_l[(3 * i + 1) * kBlock], att_l[(3 * i + 2) * kBlock]);
-          } else {
-            const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * a.n_lanes + gl];
-            if (STATS) ++coh.attr;
-            at = mk(g.x, g.y, g.z);
-          }
-          col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
-        }
-      }
+      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -1976,6 +1994,320 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The path-pool loop (FAST traversal, MODE 5): the wavefront loop with its rays
+// decoupled from lanes.  A wave holds two 64-pixel units at a time (unit slots
+// 0 and 1) - 128 paths, each one pixel's current sample - and a queue of the
+// paths whose next ray waits for traversal, in LDS.  Two phases alternate,
+// chosen with __ballot:
+//   traverse: every lane without a ray takes the next queued one - lane k of
+//             the idle lanes (mbcnt rank over the ballot of idle lanes) takes
+//             queue entry head + k, so the queue is compacted onto the idle
+//             lanes - and takes node steps; a finished traversal writes its
+//             hit to the path's LDS record and the lane takes the next ray.
+//             The phase ends when the queue is empty and fewer than
+//             wf_thresh / 64 of the lanes still traverse (the others stay
+//             suspended: node, stack, best hit kept in registers).
+//   shade:    lane q owns paths q and 64 + q (pixel q of each unit) and shades
+//             those whose hit is in (shade_step): the scattered ray, or its
+//             pixel's next camera ray, is appended to the queue (ballot +
+//             mbcnt again); a unit whose 64 paths have finished their chunk
+//             stores its chunk sums and takes the next unit from the global
+//             counter.
+// A pixel's samples still run one after another on one path, summed in order
+// by its owner lane, and every path's attenuations are stacked per path in the
+// recursion's order: images are bit-identical to render_loop's.  Rays move
+// between lanes, traversals never do (a lane keeps its ray, stack column and
+// node until the traversal ends).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPoolPaths = 128;                           // per wave: two unit slots of 64 paths
+constexpr uint32_t kBlockPaths = kPoolPaths * (kBlock / 64);   // per block
+constexpr int32_t kHitPending = -2;                            // a path's hit record before its traversal ends
+
+// One path's state, held by its owner lane: its pixel's sample under way (a path
+// whose sample reached its unit's end is done) and the depth left, packed
+// (both u16: RenderParams, raytrace.zig:102-108), the chunk's running sum.
+template <int PRNG>
+struct PathReg {
+  Rng<PRNG> rng;
+  uint32_t ds;  // depth_left << 16 | sample
+  float acc_r, acc_g, acc_b;
+  __device__ __forceinline__ uint32_t sample() const { return ds & 0xffffu; }
+  __device__ __forceinline__ uint32_t depth_left() const { return ds >> 16; }
+};
+
+// ZRT_FLAG_SCANLINES: a path's counter events go straight to its frame row
+// (paths of one unit finish at different times here); raytrace.zig:184
+__device__ __forceinline__ void scanline_add(const KArgs& a, uint32_t py, uint32_t k, uint32_t n) {
+  if (n != 0u && py < a.height) atomicAdd(&a.scanlines[3 * py + k], (unsigned long long)n);
+}
+
+// The pool's LDS: rays [6][kBlockPaths] (o.xyz, d.xyz), hits t / slot
+// [kBlockPaths], the per-wave queues [waves][kPoolPaths] of path ids.
+struct PoolLds {
+  lds_float* ray;
+  lds_float* hit_t;
+  __attribute__((address_space(3))) int32_t* hit_p;
+  __attribute__((address_space(3))) uint8_t* queue;  // this wave's
+};
+
+template <int PRNG, bool STATS, class StackT>
+__device__ __forceinline__ void render_loop_pool(const KArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the lane's traversal stack column
+  float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
+  const DevMaterial* mats = a.mats;
+  if (a.mats_in_lds) {  // block-uniform
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  }
+  const int lane = (int)__lane_id();
+  const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t wave_paths = (threadIdx.x >> 6) * kPoolPaths;  // this wave's first path in the block
+  const uint64_t g_paths = (uint64_t)blockIdx.x * kBlockPaths;  // the block's first path in the launch
+  PoolLds pl;
+  {
+    lds_float* base = (lds_float*)(lds_raw + a.lds_pool_off);
+    pl.ray = base;
+    pl.hit_t = base + 6 * kBlockPaths;
+    pl.hit_p = (__attribute__((address_space(3))) int32_t*)(base + 7 * kBlockPaths);
+    pl.queue = (__attribute__((address_space(3))) uint8_t*)(base + 8 * kBlockPaths) + wave_paths;
+  }
+  lds_float* att_base = (lds_float*)(lds_raw + a.lds_att_off);  // [row][rgb][path of the block]
+
+  // unit slots (wave-uniform): tile, chunk, the samples [.., unit_end) of the chunk
+  bool slot_on[2] = {false, false};
+  uint32_t s_lt[2] = {0xffffffffu, 0xffffffffu}, s_chunk[2] = {0, 0}, s_end[2] = {0, 0}, s_x0[2] = {0, 0},
+           s_y0[2] = {0, 0};
+  bool exhausted = false;  // the global unit counter ran out
+  PathReg<PRNG> pA, pB;    // paths lane and 64 + lane (done: sample >= the slot's unit end, 0 while it is off)
+  pA.acc_r = pA.acc_g = pA.acc_b = pB.acc_r = pB.acc_g = pB.acc_b = 0.0f;
+  pA.ds = pB.ds = 0;
+  pA.rng.init(0);
+  pB.rng.init(0);
+  uint32_t c_depth = 0, c_refl = 0, c_bg = 0;  // Progress counters (raytrace.zig:20-34) of this lane's paths
+  uint32_t q_head = 0, q_tail = 0;  // wave-uniform queue positions (mod kPoolPaths)
+
+  // the ray in flight on this lane and its suspended traversal
+  bool trav = false;
+  uint32_t cp = 0;  // its path (0 .. kPoolPaths-1 of this wave)
+  RayT r{};
+  r.rcp_det = a.tri_rcp_fast;
+  float best_t = __builtin_inff();
+  int best = -1;
+  uint32_t sp = 0;
+  const float4* q = nullptr;
+  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
+  Coh coh;  // STATS
+  uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0;
+
+  for (;;) {
+    // ---- traverse: idle lanes take queued rays; node steps
+    {
+      // shade once the queue is empty and fewer than 64 - wf_thresh lanes still traverse
+      const uint32_t thresh = 64u - a.wf_thresh;
+      WideView v{};
+      WideNode w;
+      if (trav) {
+        v = wide_view(a, r, lds_top);
+        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
+      }
+      for (;;) {
+        const uint64_t idle = __ballot(!trav);
+        const uint32_t avail = q_tail - q_head;
+        if (idle != 0ull && avail != 0u) {
+          const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+          if (!trav && rank < avail) {  // the rank-th idle lane takes queue entry head + rank
+            cp = pl.queue[(q_head + rank) & (kPoolPaths - 1u)];
+            const uint32_t P = wave_paths + cp;
+            const V3 o = mk(pl.ray[0 * kBlockPaths + P], pl.ray[1 * kBlockPaths + P], pl.ray[2 * kBlockPaths + P]);
+            const V3 d = mk(pl.ray[3 * kBlockPaths + P], pl.ray[4 * kBlockPaths + P], pl.ray[5 * kBlockPaths + P]);
+            if (STATS) ++c_rays;
+            r.ox = o.x; r.oy = o.y; r.oz = o.z;
+            r.dx = d.x; r.dy = d.y; r.dz = d.z;
+            inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
+            best_t = __builtin_inff();
+            best = -1;
+            sp = 0;
+            v = wide_view(a, r, lds_top);
+            q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+            wide_load(q, v.sx, v.sy, v.sz, w);
+            trav = true;
+          }
+          const uint32_t n_idle = (uint32_t)__builtin_popcountll(idle);
+          q_head += n_idle < avail ? n_idle : avail;
+        }
+        if (trav) {
+          if (!wide_iter<STATS, StackT, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+                                               c_sph, coh)) {
+            wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
+            const uint32_t P = wave_paths + cp;
+            pl.hit_t[P] = best_t;
+            pl.hit_p[P] = best;
+            trav = false;
+          }
+        }
+        if (STATS) c_trips += lane == 0 ? 1u : 0u;
+        const uint32_t n_trav = (uint32_t)__builtin_popcountll(__ballot(trav));
+        if (n_trav == 0u) break;
+        if (q_tail == q_head && n_trav < thresh) break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // hits written by other lanes of the wave
+    // ---- shade: owners shade their paths whose hit is in; units end and refill
+#pragma unroll 1
+    for (uint32_t s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64u + (uint32_t)lane, P = wave_paths + p;
+      const AttRows ar{att_base + P, kBlockPaths, g_paths + P, a.n_paths};
+      const uint32_t unit_end = s ? s_end[1] : s_end[0];
+      const uint32_t x0 = s ? s_x0[1] : s_x0[0], y0 = s ? s_y0[1] : s_y0[0];
+      bool push = false;
+      const uint32_t py = y0 + ((uint32_t)lane >> 3);
+      if (pA.sample() < unit_end && pl.hit_p[P] != kHitPending) {
+        if (STATS) {
+          c_lsteps += 1u;
+        }
+        V3 o = mk(pl.ray[0 * kBlockPaths + P], pl.ray[1 * kBlockPaths + P], pl.ray[2 * kBlockPaths + P]);
+        V3 d = mk(pl.ray[3 * kBlockPaths + P], pl.ray[4 * kBlockPaths + P], pl.ray[5 * kBlockPaths + P]);
+        const int hb = pl.hit_p[P];
+        const float ht = pl.hit_t[P];
+        bool path_end = false, sky = false;
+        V3 L = mk(0.0f, 0.0f, 0.0f);
+        uint32_t dl = pA.depth_left();
+        const uint32_t bg0 = c_bg, rf0 = c_refl;
+        shade_step<STATS>(a, mats, ar, pA.rng, hb, ht, o, d, dl, path_end, sky, L, c_bg, c_refl, c_shade, c_tex, coh);
+        uint32_t dh = 0;
+        if (!path_end && dl == 0) {  // the next rayColor is at depth 0: black (raytrace.zig:64-67)
+          ++c_depth;
+          dh = 1;
+          path_end = true;
+        }
+        if (a.scanlines) {
+          scanline_add(a, py, 0, dh);
+          scanline_add(a, py, 1, c_refl - rf0);
+          scanline_add(a, py, 2, c_bg - bg0);
+        }
+        uint32_t smp = pA.sample();
+        if (path_end) {
+          const V3 col = sky ? att_product<STATS>(a, ar, a.max_depth - dl, L, coh) : L;
+          pA.acc_r += col.x;
+          pA.acc_g += col.y;
+          pA.acc_b += col.z;
+          if (++smp < unit_end) {  // the pixel's next sample: jitter + Camera.getRay (raytrace.zig:173-175)
+            // (at the unit's end the path is done: its chunk's sequential sum is stored with the unit)
+            const uint32_t px = x0 + ((uint32_t)lane & 7u);
+            pA.rng.init((((uint64_t)py * a.width + px) << 16 | (uint64_t)smp) + a.seed_mix);
+            const float u = dev::div_known((float)px + rand_float(pA.rng) - 0.5f, a.f_width, a.inv_width);
+            const float vv = dev::div_known((float)py + rand_float(pA.rng) - 0.5f, a.f_height, a.inv_height);
+            o = mk(a.org[0], a.org[1], a.org[2]);
+            d = unit(sub(add(add(mk(a.llc[0], a.llc[1], a.llc[2]), scale(mk(a.hor[0], a.hor[1], a.hor[2]), u)),
+                             scale(mk(a.ver[0], a.ver[1], a.ver[2]), vv)),
+                         o));
+            dl = a.max_depth;
+            push = true;
+          }
+        } else {
+          push = true;  // the scattered ray
+        }
+        pA.ds = dl << 16 | smp;
+        if (push) {
+          pl.ray[0 * kBlockPaths + P] = o.x; pl.ray[1 * kBlockPaths + P] = o.y; pl.ray[2 * kBlockPaths + P] = o.z;
+          pl.ray[3 * kBlockPaths + P] = d.x; pl.ray[4 * kBlockPaths + P] = d.y; pl.ray[5 * kBlockPaths + P] = d.z;
+          pl.hit_p[P] = kHitPending;
+        }
+      }
+      // the unit in slot s is over: its chunk sums (one 1 KiB store), its rows' counters; the next unit
+      const bool s_on = s ? slot_on[1] : slot_on[0];
+      if (__ballot(pA.sample() < unit_end) == 0ull && (s_on || !exhausted)) {
+        const uint32_t lt = s ? s_lt[1] : s_lt[0];
+        if (s_on) {
+          const uint32_t cj = s ? s_chunk[1] : s_chunk[0];
+          a.partial[cj * a.n_slots + lt * 64u + (uint32_t)lane] = make_float4(pA.acc_r, pA.acc_g, pA.acc_b, 0.0f);
+        }
+        uint32_t u = a.total_work;
+        if (!exhausted) {
+          if (lane == 0) u = atomicAdd(a.work_counter, 1u);
+          u = __builtin_amdgcn_readfirstlane(u);
+        }
+        bool on = false;
+        uint32_t nlt = 0xffffffffu, g = 0, nx0 = 0, ny0 = 0;
+        if (u < a.total_work) {
+          const uint32_t ord = u / a.n_chunks;
+          g = u - ord * a.n_chunks;
+          nlt = a.tile_order ? a.tile_order[ord] : ord;  // costliest tiles first
+          const uint32_t t = nlt * a.world + a.rank;
+          nx0 = (t % a.tiles_x) * 8u;
+          ny0 = (t / a.tiles_x) * 8u;
+          on = true;
+        } else {
+          exhausted = true;
+        }
+        if (s) { slot_on[1] = on; s_lt[1] = nlt; s_chunk[1] = g; s_x0[1] = nx0; s_y0[1] = ny0; }
+        else { slot_on[0] = on; s_lt[0] = nlt; s_chunk[0] = g; s_x0[0] = nx0; s_y0[0] = ny0; }
+        pA.acc_r = pA.acc_g = pA.acc_b = 0.0f;
+        const uint32_t first = g * a.chunk, end = on ? min(first + a.chunk, a.spp) : 0u;
+        if (s) s_end[1] = end;
+        else s_end[0] = end;
+        pA.ds = end;  // done, unless its pixel is on the frame
+        if (on) {
+          const uint32_t px = nx0 + ((uint32_t)lane & 7u), ny = ny0 + ((uint32_t)lane >> 3);
+          // pixel q of the tile; off-frame paths stay done (finalize writes black)
+          if (px < a.xbound && ny < a.height) {
+            pA.rng.init((((uint64_t)ny * a.width + px) << 16 | (uint64_t)first) + a.seed_mix);
+            const float uu = dev::div_known((float)px + rand_float(pA.rng) - 0.5f, a.f_width, a.inv_width);
+            const float vv = dev::div_known((float)ny + rand_float(pA.rng) - 0.5f, a.f_height, a.inv_height);
+            const V3 o = mk(a.org[0], a.org[1], a.org[2]);
+            const V3 d = unit(sub(add(add(mk(a.llc[0], a.llc[1], a.llc[2]), scale(mk(a.hor[0], a.hor[1], a.hor[2]), uu)),
+                                      scale(mk(a.ver[0], a.ver[1], a.ver[2]), vv)),
+                                  o));
+            pA.ds = a.max_depth << 16 | first;
+            pl.ray[0 * kBlockPaths + P] = o.x; pl.ray[1 * kBlockPaths + P] = o.y; pl.ray[2 * kBlockPaths + P] = o.z;
+            pl.ray[3 * kBlockPaths + P] = d.x; pl.ray[4 * kBlockPaths + P] = d.y; pl.ray[5 * kBlockPaths + P] = d.z;
+            pl.hit_p[P] = kHitPending;
+            push = true;
+          }
+        }
+      }
+      // append the new rays to the queue: the rank-th pushing lane at tail + rank
+      const uint64_t pm = __ballot(push);
+      if (pm != 0ull) {
+        const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        if (push) pl.queue[(q_tail + rank) & (kPoolPaths - 1u)] = (uint8_t)p;
+        q_tail += (uint32_t)__builtin_popcountll(pm);
+      }
+      // the other path's state to the front (both slots go through the same code)
+      { PathReg<PRNG> t = pA; pA = pB; pB = t; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // rays and queue entries written by other lanes
+    if (STATS) c_loops += lane == 0 ? 1u : 0u;
+    if (!slot_on[0] && !slot_on[1] && __ballot(trav) == 0ull) break;
+  }
+
+  if (!a.scanlines) {  // (with ZRT_FLAG_SCANLINES they went to the frame rows, whose sums are the totals)
+    wave_add_u64(&a.counters[kDepthHits], c_depth);
+    wave_add_u64(&a.counters[kReflections], c_refl);
+    wave_add_u64(&a.counters[kBackground], c_bg);
+  }
+  if (STATS) {
+    wave_add_u64(&a.counters[kRays], c_rays);
+    wave_add_u64(&a.counters[kNodes], c_nodes);
+    wave_add_u64(&a.counters[kTriTests], c_tri);
+    wave_add_u64(&a.counters[kSphereTests], c_sph);
+    wave_add_u64(&a.counters[kShades], c_shade);
+    wave_add_u64(&a.counters[kTexels], c_tex);
+    wave_add_u64(&a.counters[kLeaves], c_leaves);
+    wave_add_u64(&a.counters[kReplays], c_replays);
+    wave_add_u64(&a.counters[kTravTrips], c_trips);
+    wave_add_u64(&a.counters[kLoopTrips], c_loops);
+    wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
+    coh.flush(a.counters);
+  }
+}
+
 #ifndef ZRT_ATT_ROWS_WF
 #define ZRT_ATT_ROWS_WF 4  // wavefront loop: attenuation rows kept in LDS (A/B: 2 = the lockstep kernel's)
 #endif
@@ -1983,13 +2315,22 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
 #define ZRT_WAVES_WF 4  // wavefront loop (MODE 4)
 #endif
 
+#ifndef ZRT_WAVES_POOL
+#define ZRT_WAVES_POOL 4  // path-pool loop (MODE 5)
+#endif
+#ifndef ZRT_ATT_ROWS_POOL
+#define ZRT_ATT_ROWS_POOL 1  // path-pool loop: attenuation rows kept in LDS per path (6 KiB per row per block)
+#endif
+
 template <int MODE, int PRNG, bool STATS, class StackT>
-__global__ void __launch_bounds__(kBlock, MODE == 4   ? ZRT_WAVES_WF
+__global__ void __launch_bounds__(kBlock, MODE == 5   ? ZRT_WAVES_POOL
+                                          : MODE == 4 ? ZRT_WAVES_WF
                                           : MODE == 3 ? ZRT_WAVES_WIDE
                                           : MODE == 0 ? ZRT_WAVES_LIST
                                                       : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
-  if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
+  if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT>(a);
+  else if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
   else render_loop<MODE, PRNG, STATS, StackT>(a);
 }
 
@@ -2527,7 +2868,8 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     c->origin_bound = 2.0f * H;
     const float sphere_grow = any_sphere ? float(std::ldexp(std::sqrt(2.0), -9) * (3.0 * std::sqrt(3.0) + 1.0) * double(H)) : 0.0f;
     const double tw = now_ms();
-    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f);
+    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
+                                          ZRT_SPHERE_SLOTS != 0);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
@@ -2715,6 +3057,15 @@ bool use_wavefront(const zrt_ctx* c, bool stk16) {
   (void)c;
   return !stk16;
 }
+// The path-pool loop (render_loop_pool, MODE 5) instead of the wavefront loop?
+// ZRT_POOL=0/1 forces it.
+bool use_pool(const zrt_ctx* c) {
+  if (const char* e = std::getenv("ZRT_POOL")) return std::atoi(e) != 0;
+  (void)c;
+  return false;
+}
+// LDS of the path-pool loop's rays, hits and queues per block (render_loop_pool)
+constexpr size_t kPoolLdsBytes = ((8 * sizeof(float) + 1) * kBlockPaths + 15) & ~size_t(15);
 
 template <int MODE, int PRNG, bool STATS, class StackT>
 void* kernel_ptr() {
@@ -2727,6 +3078,7 @@ void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 1) return stk16 ? kernel_ptr<1, PRNG, STATS, uint16_t>() : kernel_ptr<1, PRNG, STATS, uint32_t>();
   if (mode == 3) return stk16 ? kernel_ptr<3, PRNG, STATS, uint16_t>() : kernel_ptr<3, PRNG, STATS, uint32_t>();
   if (mode == 4) return stk16 ? kernel_ptr<4, PRNG, STATS, uint16_t>() : kernel_ptr<4, PRNG, STATS, uint32_t>();
+  if (mode == 5) return stk16 ? kernel_ptr<5, PRNG, STATS, uint16_t>() : kernel_ptr<5, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
 void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
@@ -2748,23 +3100,28 @@ void* probe_ptr(bool stk16) {
 // [row][rgb][lane] f32.  Sized so the waves per SIMD the kernel is built for
 // (its __launch_bounds__) still fit: 160 KiB / that many blocks per CU.
 struct LdsPlan {
-  uint32_t stack_rows = 0, top_off = 0, att_off = 0, att_rows = 0, mat_off = 0, mats_in_lds = 0;
+  uint32_t stack_rows = 0, top_off = 0, att_off = 0, att_rows = 0, mat_off = 0, mats_in_lds = 0, pool_off = 0;
   size_t bytes = 0;
 };
-LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf = false) {
-  const uint32_t waves = mode == 3 ? (wf ? ZRT_WAVES_WF : ZRT_WAVES_WIDE) : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
+// pool: the path-pool loop (MODE 5): its attenuation rows are per path
+// (kBlockPaths per block), and its rays / hits / queues follow them
+LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf = false,
+                 bool pool = false) {
+  const uint32_t waves = mode == 3 ? (pool ? ZRT_WAVES_POOL : wf ? ZRT_WAVES_WF : ZRT_WAVES_WIDE)
+                         : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
   // 256-thread blocks: `waves` blocks per CU; 1 KiB below the even share (a
   // block of exactly 32 KiB ran 8 % slower at 5 blocks per CU)
   const size_t budget = (160u << 10) / waves - (1u << 10);
   const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-  const size_t row_att = 3 * sizeof(float) * kBlock;
+  const size_t row_att = 3 * sizeof(float) * (pool ? kBlockPaths : kBlock);
   const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * kOctCopies : 0;
+  const size_t pool_b = pool ? kPoolLdsBytes : 0;
   // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1)
   // A/B (C4, interleaved): none 50.35, 1 row 50.57, 2 rows 50.70 Gray/s; 4 rows
   // (a 32 KiB block, the whole budget) 46.5
   // The wavefront loop runs 4 blocks per CU: its larger share holds 4 rows (its
   // scenes, the textured C5 mesh, scatter more often)
-  const uint32_t att_cap = wf ? ZRT_ATT_ROWS_WF : 2u;
+  const uint32_t att_cap = pool ? ZRT_ATT_ROWS_POOL : wf ? ZRT_ATT_ROWS_WF : 2u;
   uint32_t want = att_cap;
   if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
@@ -2772,7 +3129,7 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   if (mode == 3 && !stk16) {
     // deep trees: the stack takes what the top nodes and two attenuation rows leave
     want = std::min<uint32_t>(want, att_cap);
-    const size_t room = budget > top + want * row_att ? budget - top - want * row_att : 0;
+    const size_t room = budget > top + pool_b + want * row_att ? budget - top - pool_b - want * row_att : 0;
     L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(stack_depth, uint32_t(room / (kBlock * entry))));
   } else {
     L.stack_rows = stack_depth;  // the whole stack in LDS (16-bit FAST: it fits kStackLdsBytes)
@@ -2780,9 +3137,10 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   if (const char* f = std::getenv("ZRT_STACK_LDS_ROWS"))  // tests: force the overflow rows into use
     if (mode == 3) L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(L.stack_rows, uint32_t(std::atoi(f))));
   const size_t stack = (size_t(L.stack_rows) * kBlock * entry + 15) & ~size_t(15);
-  const size_t used = stack + top;
+  const size_t used = stack + top + pool_b;
   L.att_rows = std::min<uint32_t>(want, used < budget ? uint32_t((budget - used) / row_att) : 0u);
   L.top_off = uint32_t(stack);
+  L.pool_off = uint32_t(stack + top);
   L.att_off = uint32_t(used);
   L.bytes = used + L.att_rows * row_att;
   // the material table, if it fits what is left (ZRT_MATS_LDS=0: A/B, always global)
@@ -3087,17 +3445,26 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
     if (const char* cap = std::getenv("ZRT_DEBUG_STACK_CAP"))  // tests: a stack too small for the tree
       stack_depth = std::max<uint32_t>(4, std::min<uint32_t>(stack_depth, uint32_t(std::atoi(cap))));
-    const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
-                                       size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
-                                 : c->n_nodes < 65536;
+    bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
+                                 size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
+                           : c->n_nodes < 65536;
     // FAST: the wavefront loop (MODE 4) where lanes' traversal lengths diverge
     const bool wf = mode == 3 && p->max_depth >= 1 && zrt::use_wavefront(c, stk16);
-    void* kfn = zrt::select_kernel(wf ? 4 : mode, p->prng, diag, stk16);
+    // the path-pool loop (MODE 5) for the same cases, when asked for; a 16-bit stack
+    // must fit beside its rays and queues in the block's LDS share, else the 32-bit
+    // stack with overflow rows
+    const bool pool = mode == 3 && p->max_depth >= 1 && zrt::use_pool(c);
+    if (pool && stk16) {
+      const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
+      const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * zrt::kOctCopies : 0;
+      if (size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) + top + zrt::kPoolLdsBytes > budget) stk16 = false;
+    }
+    void* kfn = zrt::select_kernel(pool ? 5 : wf ? 4 : mode, p->prng, diag, stk16);
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf);
+    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
     int per_cu = 0;
@@ -3115,7 +3482,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint64_t n_partial = uint64_t(my_tiles) * 64u * n_chunks;
     if (c->partial.n < n_partial) c->partial.alloc(n_partial);
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
-    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_lanes;
+    // global attenuation rows: [row][lane], or [row][path] for the path-pool loop
+    const uint64_t n_paths = pool ? uint64_t(grid) * zrt::kBlockPaths : n_lanes;
+    if (n_paths >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "too many paths");
+    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_paths;
     if (att_need * sizeof(float4) > (16ull << 30))
       return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
     if (c->att.n < att_need) c->att.alloc(att_need);
@@ -3164,6 +3534,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.ref_sph = c->ref_sph.p;
     for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
     a.origin_bound = c->origin_bound;
+    {  // the camera inside the bound: so is every ray of the launch (scattered rays start at hits)
+      const float m = std::max({std::fabs(a.org[0] - a.root_c[0]), std::fabs(a.org[1] - a.root_c[1]),
+                                std::fabs(a.org[2] - a.root_c[2])});
+      a.check_origins = m <= a.origin_bound ? 0u : 1u;
+    }
     a.wnodes = c->wnodes.p;
     a.wide_stride = c->wide_stride;
     a.lds_rows = lds_rows;
@@ -3178,6 +3553,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.lds_att_off = lp.att_off;
     a.att_lds_rows = lp.att_rows;
     a.lds_mat_off = lp.mat_off;
+    a.lds_pool_off = lp.pool_off;
+    a.n_paths = uint32_t(n_paths);
     a.n_mats = c->n_mats;
     a.mats_in_lds = lp.mats_in_lds;
     a.seed_mix = p->seed * 0x9E3779B97F4A7C15ULL;
@@ -3718,6 +4095,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.ref_sph = c->ref_sph.p;
     for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
     a.origin_bound = c->origin_bound;
+    a.check_origins = 1;  // arbitrary ray origins
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
