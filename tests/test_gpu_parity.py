@@ -711,3 +711,70 @@ def test_trace_far_spheres_bit_exact(translate):
     p_ref, bad = _trace_all(scene, o, d)
     assert (p_ref >= 0).sum() > 300
     assert not bad, f"rays differing from the oracle, per traversal: {bad}"
+
+
+# ---- per-axis margins for nearly axis-parallel rays ----
+
+def _fast(scene, o, d, keep=None):
+    t_ref, p_ref = O.trace(scene, True, o, d)
+    t, p = z.trace(keep or scene, z.RenderParams(1, 1, 1, 1, traversal=z.ZRT_TRAVERSAL_FAST), o, d)
+    return int(((p != p_ref) | ~same_bits(t, t_ref)).sum()), p_ref
+
+
+def _near_parallel_rays(lo, hi, n, seed):
+    """Rays through random points of the box [lo, hi] whose direction has one
+    component 2^-40 .. 2^-6 (either sign) or exactly 0: max_k |1/d_k| from 64 to
+    inf, the rays the t-space margins turned the narrowed cull off for."""
+    rng = np.random.default_rng(seed)
+    p = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    k = rng.integers(0, 3, n)
+    tiny = (2.0 ** rng.uniform(-40, -6, n) * rng.choice([-1, 1], n)).astype(np.float32)
+    tiny[rng.random(n) < 0.1] = 0.0
+    d[np.arange(n), k] = tiny
+    o = (p - d / np.linalg.norm(d, axis=1, keepdims=True) * np.float32(rng.uniform(0.2, 2.0))
+         * np.float32(np.max(hi - lo))).astype(np.float32)
+    return o, d
+
+
+@pytest.mark.parametrize("which", [2, 3, "spheres", "bunny1e4"])
+def test_trace_per_axis_margins_every_wave_bit_exact(scenes, which, monkeypatch):
+    """The per-axis widening of wide_iter (paxis_slot) taken by EVERY wave
+    (ZRT_PAXIS_M=0) on the grazing rays of tests/grazing_rays.py, on nearly
+    axis-parallel rays and (bunny1e4) on the bunny scene moved 10^4 from the
+    origin: FAST equals the oracle bit for bit.  At the default threshold the
+    same rays take it only in waves with such a lane (the other trace tests)."""
+    monkeypatch.setenv("ZRT_PAXIS_M", "0")
+    if which == "bunny1e4":
+        import adversarial_rays as A
+        pr = A.prim_array(scenes(2).view.contents)
+        scene, o, d = A.transformed_case(O, pr, 1.0, 1e4, seed=2)
+        keep = None
+    else:
+        keep, scene, o, d = _grazing_case(scenes, which)
+    prv = prim_array(scene.contents if hasattr(scene, "contents") else scene)
+    from zraytrace_amd import _ffi
+    tri = prv[prv["kind"] == _ffi.ZRT_PRIM_TRIANGLE]
+    pts = (np.concatenate([tri["a"], tri["b"], tri["c"]]) if len(tri) else prv["center"]).reshape(-1, 3)
+    assert np.isfinite(pts).all()
+    o2, d2 = _near_parallel_rays(pts.min(0), pts.max(0), 6000, seed=11)
+    o = np.concatenate([o, o2]).astype(np.float32)
+    d = np.concatenate([d, d2]).astype(np.float32)
+    wrong, p_ref = _fast(scene, o, d, keep)
+    assert (p_ref >= 0).mean() > 0.2
+    assert wrong == 0, f"{wrong} rays differ from the oracle"
+
+
+@pytest.mark.parametrize("loop", ["wavefront", "pool"])
+def test_render_per_axis_margins_every_wave(scenes, loop, monkeypatch):
+    """The deep-tree loops with the per-axis margins in every wave
+    (ZRT_PAXIS_M=0): the teapot frame equals the oracle's bit for bit."""
+    set_loop(monkeypatch, loop)
+    monkeypatch.setenv("ZRT_PAXIS_M", "0")
+    s = scenes(3)
+    p = z.RenderParams(48, 40, 6, 20, sample_chunk=4)
+    gpu, gs = z.render(s, s.camera, p)
+    ref, rs = O.render(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k

@@ -111,6 +111,8 @@ struct KArgs {
   uint32_t n_paths;       //   paths of the launch (grid x kBlockPaths): the stride of its global attenuation rows
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
   float scene_extent;     // the triangles' largest |coordinate| (ray_slack)
+  float tri_c[3], tri_h[3];  // the triangles' bounding box: centre, half extents (paxis_grow)
+  float paxis_m;             // per-axis margins in waves with a lane of max_k |1/d_k| above this (kPaxisM)
   // Spheres (DESIGN.md §3 "Spheres"): the reference BVH nodes whose subtree holds
   // a sphere (1 byte each), and the origins the wide tree's sphere growth was
   // sized for: max_k |o_k - root_c[k]| <= origin_bound (other rays are traced the
@@ -381,6 +383,39 @@ __device__ __forceinline__ float ray_rel(float m) { return ZRT_REL_M ? 1.0000153
 // the reference boxes' slack: 2^-18 x the triangles' largest |coordinate| x m
 __device__ __forceinline__ float ray_slack(float extent, float m) {
   return ZRT_LEAF_SLACK ? __builtin_fmaxf(extent, 0x1p-100f) * 0x1p-18f * m : 0.0f;
+}
+
+// Nearly axis-parallel rays (DESIGN.md §3 "Per-axis margins").  The margins
+// above are t-space terms scaled by m = max_k |1/d_k| on every axis, but a hit's
+// excess beyond its box is a distance in space: e (t + coordinates), on axis k
+// e (t + coordinates) |1/d_k| in t.  Only an axis the ray runs (nearly) parallel
+// to needs the large term; applied to all three it turns the narrowed cull off
+// (m = 2^20: every exit x 5) and such a ray walks most of the tree.  A wave with
+// a lane whose m exceeds kPaxisM (a wave-uniform branch) therefore widens each
+// axis of every slot by its own term g |1/d_k|, g = 2^-18 (T + extent) (T: the
+// ray's farthest distance to the triangles' box, which bounds the hit's t; extent:
+// the triangles' largest |coordinate|, ray_slack's spatial term) - 6 more adds
+// per slot, for waves with such a lane only; the other waves keep ray_rel with
+// m <= kPaxisM.
+#ifndef ZRT_PAXIS
+#define ZRT_PAXIS 1  // 0: A/B only (every wave on the t-space margins of ray_rel / ray_slack)
+#endif
+#ifndef ZRT_PAXIS_LOCK
+#define ZRT_PAXIS_LOCK 0  // the lockstep loop too (its 96-VGPR budget spills 7 -> 28 registers with the branch: C4 -2.8 %)
+#endif
+#ifndef ZRT_PAXIS_LOG2M
+#define ZRT_PAXIS_LOG2M 10
+#endif
+constexpr float kPaxisM = float(1u << ZRT_PAXIS_LOG2M);
+__device__ __forceinline__ float paxis_grow(const KArgs& a, const RayT& r) {
+  const float T = (__builtin_fabsf(r.ox - a.tri_c[0]) + a.tri_h[0]) + (__builtin_fabsf(r.oy - a.tri_c[1]) + a.tri_h[1]) +
+                  (__builtin_fabsf(r.oz - a.tri_c[2]) + a.tri_h[2]);  // >= the L2 distance to any corner
+  return (T + __builtin_fmaxf(a.scene_extent, 0x1p-100f)) * 0x1.0001p-18f;  // (rounding of T: the extra 2^-16)
+}
+// the per-axis term in t, finite (an infinite 1/d_k keeps the slab's exact +-inf:
+// the reference's own test then rejects every leaf off the plane)
+__device__ __forceinline__ float paxis_t(float g, float inv) {
+  return __builtin_fminf(g * __builtin_fabsf(inv), 0x1p126f);
 }
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
@@ -875,7 +910,7 @@ __device__ __forceinline__ bool static_ok(float nx, float ny, float nz, float fx
 // recomputed from the node in memory (the same two roundings as the packed
 // form) so that none of them stays live across the node.
 __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, const RayT& r, float tb,
-                                           bool sx, bool sy, bool sz) {
+                                           bool sx, bool sy, bool sz, float& entry) {
   const float t_min = 0.001f;
   const float* f = reinterpret_cast<const float*>(q) + k;
 #if ZRT_OCT_COPIES
@@ -888,6 +923,8 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   const float nx = (f[px] - r.ox) * r.ix, fx = (f[qx] - r.ox) * r.ix;
   const float ny = (f[py] - r.oy) * r.iy, fy = (f[qy] - r.oy) * r.iy;
   const float nz = (f[pz] - r.oz) * r.iz, fz = (f[qz] - r.oz) * r.iz;
+  // the exact loose entry (the order-hazard test's E; wide_iter's en when its slabs are not widened)
+  entry = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, t_min));
   if (!ZRT_GRAZE_SLACK)
     return (__builtin_fminf(fx, tb) > __builtin_fmaxf(nx, t_min)) &&
            (__builtin_fminf(fy, tb) > __builtin_fmaxf(ny, t_min)) &&
@@ -913,7 +950,7 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
 // static_ok of leaf slot k, its slab distances recomputed from the node in memory
 // (the same two roundings as wide_iter's) so that none stays live across the node
 template <class FP>
-__device__ __forceinline__ bool static_ok_at(FP f, const RayT& r, bool sx, bool sy, bool sz) {
+__device__ __forceinline__ bool static_ok_at(FP f, const RayT& r, bool sx, bool sy, bool sz, float& entry) {
 #if ZRT_OCT_COPIES
   (void)sx; (void)sy; (void)sz;
   const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
@@ -921,20 +958,21 @@ __device__ __forceinline__ bool static_ok_at(FP f, const RayT& r, bool sx, bool 
   const int px = sx ? 12 : 0, py = sy ? 16 : 4, pz = sz ? 20 : 8;
   const int qx = sx ? 0 : 12, qy = sy ? 4 : 16, qz = sz ? 8 : 20;
 #endif
-  return static_ok((f[px] - r.ox) * r.ix, (f[py] - r.oy) * r.iy, (f[pz] - r.oz) * r.iz, (f[qx] - r.ox) * r.ix,
-                   (f[qy] - r.oy) * r.iy, (f[qz] - r.oz) * r.iz);
+  const float nx = (f[px] - r.ox) * r.ix, ny = (f[py] - r.oy) * r.iy, nz = (f[pz] - r.oz) * r.iz;
+  entry = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, 0.001f));  // the exact loose entry
+  return static_ok(nx, ny, nz, (f[qx] - r.ox) * r.ix, (f[qy] - r.oy) * r.iy, (f[qz] - r.oz) * r.iz);
 }
 // (q is a generic pointer: a node of the top levels lives in LDS - the root,
 // which holds the ground sphere's leaf in every reference scene - and is read
 // with ds_read, not a flat load through the vector memory path)
 __device__ __forceinline__ bool static_ok_slot(const float4* __restrict__ q, int k, const RayT& r, bool sx, bool sy,
-                                               bool sz) {
+                                               bool sz, float& entry) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (__builtin_amdgcn_is_shared(reinterpret_cast<const void*>(q)))
     return static_ok_at((const __attribute__((address_space(3))) float*)(reinterpret_cast<const float*>(q)) + k, r,
-                        sx, sy, sz);
+                        sx, sy, sz, entry);
 #endif
-  return static_ok_at(reinterpret_cast<const float*>(q) + k, r, sx, sy, sz);
+  return static_ok_at(reinterpret_cast<const float*>(q) + k, r, sx, sy, sz, entry);
 }
 
 constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
@@ -1046,7 +1084,7 @@ __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const Wid
 // the order-hazard test of wide_finish follows).  Its state between calls is
 // (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
-template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES>
+template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
                                           const float4*& q, uint32_t& sp, float& best_t, int& best,
@@ -1067,38 +1105,55 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
-  const f2 nx01 = ZRT_SLAB_X(w.nx, x, y), nx23 = ZRT_SLAB_X(w.nx, z, w);
-  const f2 ny01 = ZRT_SLAB_Y(w.ny, x, y), ny23 = ZRT_SLAB_Y(w.ny, z, w);
-  const f2 nz01 = ZRT_SLAB_Z(w.nz, x, y), nz23 = ZRT_SLAB_Z(w.nz, z, w);
-  const f2 fx01 = ZRT_SLAB_X(w.fx, x, y), fx23 = ZRT_SLAB_X(w.fx, z, w);
-  const f2 fy01 = ZRT_SLAB_Y(w.fy, x, y), fy23 = ZRT_SLAB_Y(w.fy, z, w);
-  const f2 fz01 = ZRT_SLAB_Z(w.fz, x, y), fz23 = ZRT_SLAB_Z(w.fz, z, w);
+  f2 nx01 = ZRT_SLAB_X(w.nx, x, y), nx23 = ZRT_SLAB_X(w.nx, z, w);
+  f2 ny01 = ZRT_SLAB_Y(w.ny, x, y), ny23 = ZRT_SLAB_Y(w.ny, z, w);
+  f2 nz01 = ZRT_SLAB_Z(w.nz, x, y), nz23 = ZRT_SLAB_Z(w.nz, z, w);
+  f2 fx01 = ZRT_SLAB_X(w.fx, x, y), fx23 = ZRT_SLAB_X(w.fx, z, w);
+  f2 fy01 = ZRT_SLAB_Y(w.fy, x, y), fy23 = ZRT_SLAB_Y(w.fy, z, w);
+  f2 fz01 = ZRT_SLAB_Z(w.fz, x, y), fz23 = ZRT_SLAB_Z(w.fz, z, w);
 #undef ZRT_SLAB_X
 #undef ZRT_SLAB_Y
 #undef ZRT_SLAB_Z
-  const SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
-  const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
-  const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
-  const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
+  // a lane of the wave runs nearly parallel to an axis (paxis_grow): every slab
+  // widened in place by its axis's own term; the leaf slots' exact intervals (the
+  // reference's loose test, the hazard entry) are then recomputed by loose_slot
+  bool pw = false;
+  if (ZRT_PAXIS && PAXIS && __builtin_expect(__ballot(m > a.paxis_m) != 0ull, 0)) {
+    pw = true;
+    const float g = paxis_grow(a, r);
+    const float gx = paxis_t(g, r.ix), gy = paxis_t(g, r.iy), gz = paxis_t(g, r.iz);
+    nx01.x -= gx; nx01.y -= gx; nx23.x -= gx; nx23.y -= gx;
+    ny01.x -= gy; ny01.y -= gy; ny23.x -= gy; ny23.y -= gy;
+    nz01.x -= gz; nz01.y -= gz; nz23.x -= gz; nz23.y -= gz;
+    fx01.x += gx; fx01.y += gx; fx23.x += gx; fx23.y += gx;
+    fy01.x += gy; fy01.y += gy; fy23.x += gy; fy23.y += gy;
+    fz01.x += gz; fz01.y += gz; fz23.x += gz; fz23.y += gz;
+  }
+  SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
+  SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
+  SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
+  SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
   // narrowed test: entry > exit * rel (+ slack for a leaf slot) culls (ray_slack:
-  // inner slots' boxes are stored grown, leaf slots' are the reference leaves')
-  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, rel, r0 < 0 ? slk : 0.0f));
-  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, rel, r1 < 0 ? slk : 0.0f));
-  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, rel, r2 < 0 ? slk : 0.0f));
-  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, rel, r3 < 0 ? slk : 0.0f));
+  // inner slots' boxes are stored grown, leaf slots' are the reference leaves');
+  // widened slabs carry their margins already (rounding: 2^-16)
+  const float rl = pw ? 1.0000153f : rel, sl = pw ? 0.0f : slk;
+  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, rl, r0 < 0 ? sl : 0.0f));
+  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, rl, r1 < 0 ? sl : 0.0f));
+  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, rl, r2 < 0 ? sl : 0.0f));
+  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, rl, r3 < 0 ? sl : 0.0f));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
   }
   // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
   bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
-  const bool w0 = o0 && !(s0.en < s0.ex), w1 = o1 && !(s1.en < s1.ex);
-  const bool w2 = o2 && !(s2.en < s2.ex), w3 = o3 && !(s3.en < s3.ex);
+  const bool w0 = o0 && (pw || !(s0.en < s0.ex)), w1 = o1 && (pw || !(s1.en < s1.ex));
+  const bool w2 = o2 && (pw || !(s2.en < s2.ex)), w3 = o3 && (pw || !(s3.en < s3.ex));
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz);
-    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz);
-    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz);
-    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz);
+    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en);
+    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en);
+    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz, s2.en);
+    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz, s3.en);
   }
 #if ZRT_SPHERE_SLOTS
   // leaf slots holding a sphere (ref a - 2^30, accel_build.hpp): opened when the
@@ -1108,11 +1163,22 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   // test nor the current best may cull them; every sphere hit of a static-ok
   // leaf is then seen, and the order-hazard tests see it too.  (A wave-uniform
   // branch: nodes with sphere leaves are few.)
+  // The slot's interval in registers settles most: en < ex (the narrowed interval
+  // is not empty: every axis passes) opens it, ex <= t_min (an axis's far plane
+  // at or behind t_min: that axis fails; tb > t_min) keeps it shut; the rest, and
+  // every slot of a widened wave (pw), take the per-axis test from memory.
   if (__builtin_expect(__ballot(min(min(r0, r1), min(r2, r3)) < -kSphereSlotBias) != 0ull, 0)) {
-    if (r0 < -kSphereSlotBias) { o0 = static_ok_slot(q, 0, r, sx, sy, sz); r0 += kSphereSlotBias; }
-    if (r1 < -kSphereSlotBias) { o1 = static_ok_slot(q, 1, r, sx, sy, sz); r1 += kSphereSlotBias; }
-    if (r2 < -kSphereSlotBias) { o2 = static_ok_slot(q, 2, r, sx, sy, sz); r2 += kSphereSlotBias; }
-    if (r3 < -kSphereSlotBias) { o3 = static_ok_slot(q, 3, r, sx, sy, sz); r3 += kSphereSlotBias; }
+#define ZRT_SPHERE_SLOT(K)                                                                    \
+  if (r##K < -kSphereSlotBias) {                                                              \
+    o##K = !pw && s##K.en < s##K.ex;                                                          \
+    if (!o##K && s##K.ex > 0.001f) o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);       \
+    r##K += kSphereSlotBias;                                                                  \
+  }
+    ZRT_SPHERE_SLOT(0)
+    ZRT_SPHERE_SLOT(1)
+    ZRT_SPHERE_SLOT(2)
+    ZRT_SPHERE_SLOT(3)
+#undef ZRT_SPHERE_SLOT
   }
 #endif
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
@@ -1280,7 +1346,7 @@ __device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, Stack
   }
 }
 
-template <bool STATS, class StackT>
+template <bool STATS, class StackT, bool PAXIS = ZRT_PAXIS_LOCK>
 __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                               const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
                                               int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
@@ -1291,7 +1357,8 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
   WideNode w;
   wide_load(q, v.sx, v.sy, v.sz, w);
-  while (wide_iter<STATS, StackT>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph, coh)) {
+  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves,
+                                                           c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
@@ -1879,7 +1946,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       for (;;) {
         if (trav) {
           // (its lanes' nodes are rarely one: no scalar-load test, C5 -1.4 % with it)
-          if (!wide_iter<STATS, StackT, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, false, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             trav = false;
@@ -2141,7 +2208,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, false, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
@@ -2373,7 +2440,8 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   } else if (MODE == 3) {
     uint32_t c_replays = 0;
     Coh coh;
-    traverse_wide<false>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
+    traverse_wide<false, StackT, true>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays,
+                                       coh);
   } else {
     traverse_bvh<MODE == 1, false>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
   }
@@ -2702,6 +2770,7 @@ struct zrt_ctx {
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
+  float tri_c[3] = {0.0f, 0.0f, 0.0f}, tri_h[3] = {0.0f, 0.0f, 0.0f};  // KArgs::tri_c / tri_h
   zrt::DevBuf<float4> att;
   zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
@@ -2751,6 +2820,7 @@ struct HostScene {
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;  // KArgs::tri_rcp_fast
   float scene_extent = 0.0f;  // KArgs::scene_extent
+  float tri_c[3] = {0.0f, 0.0f, 0.0f}, tri_h[3] = {0.0f, 0.0f, 0.0f};  // KArgs::tri_c / tri_h
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;  // KArgs::root_c / origin_bound
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
@@ -2899,11 +2969,18 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   }
   std::vector<float4> prims(3 * size_t(slot_to_prim.size()));
   std::vector<float4> shade(slot_to_prim.size());
+  double tlo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, thi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
     const zrt_prim& p = s->prims[slot_to_prim[sl]];
     if (p.kind == ZRT_PRIM_TRIANGLE)  // ray_slack: the triangles' largest |coordinate|
-      for (const auto& v : {p.a, p.b, p.c})
+      for (const auto& v : {p.a, p.b, p.c}) {
         c->scene_extent = std::max({c->scene_extent, std::fabs(v.x), std::fabs(v.y), std::fabs(v.z)});
+        const double vk[3] = {v.x, v.y, v.z};
+        for (int k = 0; k < 3; ++k) {  // (NaN coordinates: the box becomes NaN, paxis_grow infinite)
+          tlo[k] = vk[k] < tlo[k] || vk[k] != vk[k] ? vk[k] : tlo[k];
+          thi[k] = vk[k] > thi[k] || vk[k] != vk[k] ? vk[k] : thi[k];
+        }
+      }
     float4* q = &prims[3 * sl];
     float4& sh = shade[sl];
     uint32_t tag = p.material;
@@ -2930,6 +3007,18 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       sh = make_float4(1.0f / p.radius, 0.0f, 0.0f, 0.0f);  // sphere.zig:46 scale(1.0/radius)
     }
     std::memcpy(&sh.w, &tag, 4);
+  }
+  // the triangles' bounding box as centre and half extents, rounded so that the
+  // f32 box contains the exact one (paxis_grow); no triangle: an empty box at 0
+  for (int k = 0; k < 3; ++k) {
+    if (!(tlo[k] <= thi[k])) {
+      if (tlo[k] == HUGE_VAL) tlo[k] = thi[k] = 0.0;  // no triangles
+      else { c->tri_c[k] = 0.0f; c->tri_h[k] = HUGE_VALF; continue; }  // NaN
+    }
+    const double ctr = 0.5 * tlo[k] + 0.5 * thi[k];
+    c->tri_c[k] = float(ctr);
+    const double h = std::max(thi[k] - double(c->tri_c[k]), double(c->tri_c[k]) - tlo[k]);
+    c->tri_h[k] = std::nextafter(float(h), HUGE_VALF);
   }
   // materials + textures.  An image whose every value is exactly k/255 (what
   // png_image.zig:76-89 produces) is stored as 8-bit RGBX and expanded through
@@ -3042,6 +3131,10 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->texel_bytes = h.texel_bytes;
   c->tri_rcp_fast = h.tri_rcp_fast;
   c->scene_extent = h.scene_extent;
+  for (int k = 0; k < 3; ++k) {
+    c->tri_c[k] = h.tri_c[k];
+    c->tri_h[k] = h.tri_h[k];
+  }
   c->slot_to_prim = h.slot_to_prim;
 }
 
@@ -3056,6 +3149,12 @@ bool use_wavefront(const zrt_ctx* c, bool stk16) {
   if (const char* e = std::getenv("ZRT_WF")) return std::atoi(e) != 0;
   (void)c;
   return !stk16;
+}
+// Per-axis margins (wide_iter) in waves with a lane whose max_k |1/d_k| exceeds
+// this; ZRT_PAXIS_M overrides (the tests set 0: every wave takes them)
+float paxis_threshold() {
+  if (const char* e = std::getenv("ZRT_PAXIS_M")) return float(std::atof(e));
+  return kPaxisM;
 }
 // The path-pool loop (render_loop_pool, MODE 5) instead of the wavefront loop?
 // ZRT_POOL=0/1 forces it.
@@ -3528,6 +3627,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
     a.scene_extent = c->scene_extent;
+    a.paxis_m = zrt::paxis_threshold();
+    for (int k = 0; k < 3; ++k) {
+      a.tri_c[k] = c->tri_c[k];
+      a.tri_h[k] = c->tri_h[k];
+    }
     a.stack_depth = stack_depth;
     a.ref_stack = std::min(c->stack_depth, stack_depth);
     a.leaf_of_slot = c->leaf_of_slot.p;
@@ -4089,6 +4193,11 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
     a.scene_extent = c->scene_extent;
+    a.paxis_m = zrt::paxis_threshold();
+    for (int k = 0; k < 3; ++k) {
+      a.tri_c[k] = c->tri_c[k];
+      a.tri_h[k] = c->tri_h[k];
+    }
     a.stack_depth = stack_depth;
     a.ref_stack = c->stack_depth;
     a.leaf_of_slot = c->leaf_of_slot.p;
