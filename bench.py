@@ -379,6 +379,15 @@ def main():
                 wb["pmc_wrreq_32B"] = int(n32)
                 wb["pmc_wrreq_bytes"] = int(64 * n64 + 32 * n32)
         roof["write_budget"] = wb
+        # SIMD efficiency of the loop (STATS launch, zrt_ctx_debug_counters slots 4 / 21-23):
+        # lane node visits / (64 x the wave's traversal trips), and the lanes that ran a
+        # rayColor step / (64 x loop iterations that ran one)
+        loops = {0: "list", 1: "binary", 2: "reference", 3: "lockstep", 4: "wavefront", 5: "path pool"}
+        simd = {"sampling_loop": loops.get(int(st.get("sampling_loop", -1)), "unknown")}
+        if int(dc[21]):
+            simd["traversal_lane_eff"] = round(int(dc[4]) / (64.0 * int(dc[21])), 4)
+        if int(dc[22]):
+            simd["shade_lane_eff"] = round(int(dc[23]) / (64.0 * int(dc[22])), 4)
         roof["kernel"] = f"render_kernel (BVH {args.traversal} traversal)"
         roof["counters_from"] = f"one untimed ZRT_FLAG_STATS launch (kernel {diag_kernel_ms:.1f} ms)"
         out = {
@@ -406,6 +415,7 @@ def main():
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 4),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 2),
             "order_replays": diag["order_replays"],
+            "simd": simd,
             "roofline": roof,
             "accel": {"reference_bvh_nodes": diag["bvh_nodes"], "reference_bvh_depth": diag["bvh_max_depth"],
                       "wide_nodes": diag["wide_nodes"], "node_bytes": diag["node_bytes"]},

@@ -218,6 +218,10 @@ typedef struct zrt_stats {
   float box_excess_max_triangle;
   float box_excess_max_sphere;
   uint64_t box_excess_hits;
+  /* the sampling loop of the last launch: 0 surface list, 1
+   * binary / 2 reference BVH traversal, FAST traversal: 3 lockstep, 4 wavefront,
+   * 5 path pool */
+  uint32_t sampling_loop;
 } zrt_stats;
 
 /* One frame row's share of the Progress counters (raytrace.zig:20-34): what

@@ -94,7 +94,8 @@ class Stats(C.Structure):
                 ("node_bytes", C.c_uint32), ("wide_nodes", C.c_uint32),
                 ("texel_bytes", C.c_uint32), ("schedule_ms", C.c_float),
                 ("order_replays", C.c_uint64), ("box_excess_max_triangle", C.c_float),
-                ("box_excess_max_sphere", C.c_float), ("box_excess_hits", C.c_uint64)]
+                ("box_excess_max_sphere", C.c_float), ("box_excess_hits", C.c_uint64),
+                ("sampling_loop", C.c_uint32)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -679,8 +679,11 @@ struct ExcessAcc {
 // (KArgs::origin_bound, DESIGN.md §3 "Spheres"); other rays (none in a render of
 // the reference's scenes: their cameras lie inside that region) are traced the
 // reference's way alone.
+#ifndef ZRT_ORIGIN_CHECK
+#define ZRT_ORIGIN_CHECK 1  // A/B only: 0 drops the check (not exact for origins outside the bound)
+#endif
 __device__ __forceinline__ bool ray_origin_ok(const KArgs& a, const RayT& r) {
-  if (!a.check_origins) return true;  // (wave-uniform: a scalar branch)
+  if (!ZRT_ORIGIN_CHECK || !a.check_origins) return true;  // (wave-uniform: a scalar branch)
   const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox - a.root_c[0]), __builtin_fabsf(r.oy - a.root_c[1])),
                                   __builtin_fabsf(r.oz - a.root_c[2]));
   return m <= a.origin_bound;
@@ -1331,18 +1334,17 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 template <bool STATS, class StackT>
 __device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, StackT* __restrict__ stk, uint32_t gl,
                                             float& best_t, int& best, uint32_t& c_replays) {
-  if (__builtin_expect(ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best), 0)) {
+  // an origin farther out than the sphere growth was sized for: the reference's
+  // way alone (narrow = false).  One call site for both cases: the replay is
+  // inlined, and a second copy cost the lockstep loop 2.8 % on C4 (registers).
+  const bool far = __builtin_expect(!ray_origin_ok(a, r), 0);
+  if (__builtin_expect((ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best)) || far, 0)) {
     if (STATS) ++c_replays;
 #if ZRT_REPLAY_OFF
-    best_t = -best_t;  // A/B only: the replay's cost without its code (results not exact)
-#else
-    reference_replay<StackT>(a, r, stk, gl, best_t, best);
+    if (!far) best_t = -best_t;  // A/B only: the replay's cost without its code (results not exact)
+    else
 #endif
-  }
-  // an origin farther out than the sphere growth was sized for: the reference's way alone
-  if (__builtin_expect(!ray_origin_ok(a, r), 0)) {
-    if (STATS) ++c_replays;
-    reference_replay<StackT>(a, r, stk, gl, best_t, best, false);
+    reference_replay<StackT>(a, r, stk, gl, best_t, best, !far);
   }
 }
 
@@ -2797,6 +2799,7 @@ struct zrt_ctx {
   uint32_t last_tiles = 0, last_rank = 0, last_world = 1, last_tiles_x = 0, last_xbound = 0;
   bool last_stats = false;
   int last_mode = 0;
+  int last_loop = 0;  // zrt_stats::sampling_loop
   int cu_count = 0;
   ~zrt_ctx() {
     if (ev_pre) (void)hipEventDestroy(ev_pre);
@@ -3157,11 +3160,14 @@ float paxis_threshold() {
   return kPaxisM;
 }
 // The path-pool loop (render_loop_pool, MODE 5) instead of the wavefront loop?
-// ZRT_POOL=0/1 forces it.
-bool use_pool(const zrt_ctx* c) {
+// ZRT_POOL=0/1 forces it.  Default: the wavefront loop's cases (trees past the
+// 16-bit stack), where it is 4 % faster at C5's full size (8.30 -> 8.65 Gray/s,
+// profiles/r03/ab5); on the teapot (C3) and the bunny (C4) the lockstep loop
+// stays ahead (14.7 vs 14.3, 50.5 vs 29.4 Gray/s).
+bool use_pool(const zrt_ctx* c, bool stk16) {
   if (const char* e = std::getenv("ZRT_POOL")) return std::atoi(e) != 0;
   (void)c;
-  return false;
+  return !stk16;
 }
 // LDS of the path-pool loop's rays, hits and queues per block (render_loop_pool)
 constexpr size_t kPoolLdsBytes = ((8 * sizeof(float) + 1) * kBlockPaths + 15) & ~size_t(15);
@@ -3552,7 +3558,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // the path-pool loop (MODE 5) for the same cases, when asked for; a 16-bit stack
     // must fit beside its rays and queues in the block's LDS share, else the 32-bit
     // stack with overflow rows
-    const bool pool = mode == 3 && p->max_depth >= 1 && zrt::use_pool(c);
+    const bool pool = mode == 3 && p->max_depth >= 1 && zrt::use_pool(c, stk16);
     if (pool && stk16) {
       const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
       const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * zrt::kOctCopies : 0;
@@ -3727,6 +3733,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_xbound = g.xbound;
     c->last_stats = diag;
     c->last_mode = mode;
+    c->last_loop = pool ? 5 : wf ? 4 : mode;
     c->launched = 1;
     return ZRT_OK;
   }
@@ -3771,6 +3778,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->box_excess_hits = h[zrt::kExcessHits];
     out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
     out->wide_nodes = c->n_wide;
+    out->sampling_loop = uint32_t(c->last_loop);
     out->texel_bytes = c->texel_bytes;
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
