@@ -21,4 +21,9 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   timeout -s KILL 400 rocprofv3 --pmc $grp --output-format csv -d $O/pmc$i -o run -- python $B --steps 1 --warmup 0 > $O/pmc$i.json 2> $O/pmc$i.err || { echo "pmc pass $i ($grp) failed"; tail -3 $O/pmc$i.err; exit 1; }
 done
-python $R/tools/pmc_summary.py $O > $O/entry.json && echo pmc-done
+python $R/tools/pmc_summary.py $O > $O/entry.json || exit 1
+# gpurun copies back at most 64 MiB: keep the summaries, compress the raw CSVs
+# (the BVH build's radix-sort launches make a million-triangle scene's large)
+find $O -name '*.csv' ! -name '*kernel_stats.csv' -size +1M -exec gzip -9 {} \;
+find $O -name '*.csv.gz' -size +8M -delete
+echo pmc-done
