@@ -6,7 +6,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${1:-dist}; mkdir -p $O
 export MASTER_ADDR=127.0.0.1
 A="--scene 3 --width 1024 --height 1024 --spp 256 --depth 20 --no-cpu-baseline"
-show() { python -c "import json; d=json.load(open('$1')); print(d['n_gpus'], d['value'], d['frame_sha1'][:12], d['frame_equal_to_n1'], d['per_rank_ms'])"; }
+# (gloo prints its connection lines to stdout too: the bench line is the last '{' line)
+show() { python -c "import json; d=json.loads([l for l in open('$1') if l.startswith('{')][-1]); print(d['n_gpus'], d['value'], d['frame_sha1'][:12], d['frame_equal_to_n1'], d['per_rank_ms'])"; }
 timeout -k 10 300 python $R/bench.py $A > $O/n1.json 2> $O/n1.err && show $O/n1.json && \
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
   $R/bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo --device 0 $A > $O/n2.json 2> $O/n2.err && show $O/n2.json && \
