@@ -228,6 +228,12 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
         w.child[w.count++] = N[opened].right;
       }
     }
+    // leaf children holding a sphere first (render.hip tests slot 0 alone for
+    // a node with sphere slots); slot order never changes a result: hits are
+    // ranked by t and primitive slot, children visited near-first
+    if (mark_spheres)
+      std::stable_partition(w.child, w.child + w.count,
+                            [&](int32_t c) { return N[size_t(c)].leaf >= 0 && N[size_t(c)].sphere; });
     wide_of[bn] = int32_t(wide.size());
     wide.push_back(w);
     return wide_of[bn];

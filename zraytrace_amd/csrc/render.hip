@@ -894,6 +894,9 @@ __device__ __forceinline__ SlotT slot_interval(float nx, float ny, float nz, flo
   s.ex = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tb));
   return s;
 }
+#ifndef ZRT_SPHERE_FIRST
+#define ZRT_SPHERE_FIRST 1  // A/B: 0 looks for sphere slots in all four slots of every node
+#endif
 #ifndef ZRT_SPHERE_SLOTS
 #define ZRT_SPHERE_SLOTS 1  // A/B only: 0 culls sphere leaves like triangle leaves (not exact, DESIGN.md §3 "Spheres")
 #endif
@@ -1170,7 +1173,11 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   // is not empty: every axis passes) opens it, ex <= t_min (an axis's far plane
   // at or behind t_min: that axis fails; tb > t_min) keeps it shut; the rest, and
   // every slot of a widened wave (pw), take the per-axis test from memory.
+#if ZRT_SPHERE_FIRST  // accel_build puts a node's sphere leaves in its first slots
+  if (__builtin_expect(__ballot(r0 < -kSphereSlotBias) != 0ull, 0)) {
+#else
   if (__builtin_expect(__ballot(min(min(r0, r1), min(r2, r3)) < -kSphereSlotBias) != 0ull, 0)) {
+#endif
 #define ZRT_SPHERE_SLOT(K)                                                                    \
   if (r##K < -kSphereSlotBias) {                                                              \
     o##K = !pw && s##K.en < s##K.ex;                                                          \
@@ -2377,6 +2384,9 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   }
 }
 
+#ifndef ZRT_ATT_ROWS_LIST
+#define ZRT_ATT_ROWS_LIST 8  // list loop (MODE 0): attenuation rows kept in LDS (as many as its 6-block share holds)
+#endif
 #ifndef ZRT_ATT_ROWS_WF
 #define ZRT_ATT_ROWS_WF 4  // wavefront loop: attenuation rows kept in LDS (A/B: 2 = the lockstep kernel's)
 #endif
@@ -3226,7 +3236,9 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   // (a 32 KiB block, the whole budget) 46.5
   // The wavefront loop runs 4 blocks per CU: its larger share holds 4 rows (its
   // scenes, the textured C5 mesh, scatter more often)
-  const uint32_t att_cap = pool ? ZRT_ATT_ROWS_POOL : wf ? ZRT_ATT_ROWS_WF : 2u;
+  // The list loop (mode 0: no stack, no tree in LDS) keeps up to 8 rows: C2 (depth
+  // 30, glass) 32.7 -> 33.3 (4 rows) -> 34.0 Gray/s (8 rows), profiles/r03/ab12
+  const uint32_t att_cap = pool ? ZRT_ATT_ROWS_POOL : wf ? ZRT_ATT_ROWS_WF : mode == 0 ? ZRT_ATT_ROWS_LIST : 2u;
   uint32_t want = att_cap;
   if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
