@@ -7,6 +7,8 @@
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$TAG; mkdir -p $O
+(cd $R && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1) || { echo "smoke failed"; tail -5 $O/smoke.txt; exit 1; }
+tail -1 $O/smoke.txt
 if [ "$1" == "--pmc-c5" ]; then
   shift
   bash $R/tools/gpu_pmc.sh $TAG/pmc_c5 --scene 6 --width 4096 --height 4096 --spp 4096 --depth 20 --steps 1 --warmup 0 || exit 1
