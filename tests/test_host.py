@@ -257,3 +257,16 @@ def test_binary_scene_rejects(tmp_path):
     with pytest.raises(z.ZrtError) as e:
         z.LoadedScene.read(str(tmp_path / "missing.zrts"))
     assert e.value.code == _ffi.ZRT_E_IO
+
+
+def test_stats_struct_matches_header():
+    """zraytrace_amd._ffi.Stats lists zrt_stats's fields (include/zrt.h) in order, so
+    a field added to the C struct cannot shift the ctypes layout unnoticed."""
+    import re
+    with open(os.path.join(REPO, "include", "zrt.h")) as f:
+        h = f.read()
+    body = h[h.index("typedef struct zrt_stats {"):h.index("} zrt_stats;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"\b(?:u?int(?:32|64)_t|float|double)\s+(\w+)\s*;", body)
+    assert names == [n for n, _ in _ffi.Stats._fields_]
+
