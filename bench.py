@@ -387,6 +387,8 @@ def main():
         if int(dc[21]):
             simd["traversal_lane_eff"] = round(int(dc[4]) / (64.0 * int(dc[21])), 4)
         if int(dc[22]):
+            # (the path pool's lanes own two paths each and may shade both in one
+            # loop iteration: there the ratio runs up to 2)
             simd["shade_lane_eff"] = round(int(dc[23]) / (64.0 * int(dc[22])), 4)
         roof["kernel"] = f"render_kernel (BVH {args.traversal} traversal)"
         roof["counters_from"] = f"one untimed ZRT_FLAG_STATS launch (kernel {diag_kernel_ms:.1f} ms)"
