@@ -230,6 +230,12 @@ def cpu_baseline(scene, scene_index, depth, target_s=15.0):
                       f"{st['rays_processed']} rays in {dt:.2f} s on 1 core (BVH build "
                       f"{st['preprocess_ms'] / 1e3:.2f} s excluded)",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            # the one-core rate scaled linearly to every core of the box - an upper
+            # bound for the single-threaded reference (it has no threads), labelled as such
+            "all_cores_linear": {"value": round(st["rays_processed"] / dt / 1e6 * (os.cpu_count() or 1), 3),
+                                 "unit": "Mrays/s", "cores": os.cpu_count(),
+                                 "note": "linear extrapolation of the 1-core figure (not measured; the reference "
+                                         "is single-threaded)"},
             "c1_full": {"config": "scene 1 (7 spheres, list), 256x256 @ 16 spp, depth 30, reference RNG stream",
                         "rays": c1["rays_processed"], "seconds": round(c1_s, 3),
                         "mrays_per_s": round(c1["rays_processed"] / c1_s / 1e6, 3), "cores": 1}}
@@ -319,7 +325,9 @@ def main():
 
     st = fr.ctx.stats()  # Progress counters of the last timed launch (identical every step)
     # per-rank kernel and gather times of the timed steps (HIP events on the frame's stream)
-    my_times = [sum(kernel_ms) / len(kernel_ms), sum(fr.gather_ms) / max(1, len(fr.gather_ms))]
+    # (gather_ms holds the timed steps' gathers; None rather than a fake 0 if it has none)
+    my_times = [sum(kernel_ms) / len(kernel_ms),
+                sum(fr.gather_ms) / len(fr.gather_ms) if fr.gather_ms else float("nan")]
     frame_sha1 = hashlib.sha1(fr.image().tobytes()).hexdigest() if rank == 0 else None
     # Traffic diagnostics (node visits, primitive tests, ...) come from one extra,
     # untimed launch of the diagnostic kernel flavour: same traversal, same image.
@@ -383,7 +391,9 @@ def main():
         # lane node visits / (64 x the wave's traversal trips), and the lanes that ran a
         # rayColor step / (64 x loop iterations that ran one)
         loops = {0: "list", 1: "binary", 2: "reference", 3: "lockstep", 4: "wavefront", 5: "path pool"}
-        simd = {"sampling_loop": loops.get(int(st.get("sampling_loop", -1)), "unknown")}
+        # (an A/B variant built before zrt_stats.sampling_loop existed leaves it zero: "unknown", not "list")
+        simd = {"sampling_loop": loops.get(int(st.get("sampling_loop", -1)), "unknown") if bid != "unknown"
+                else "unknown"}
         if int(dc[21]):
             simd["traversal_lane_eff"] = round(int(dc[4]) / (64.0 * int(dc[21])), 4)
         if int(dc[22]):
@@ -425,7 +435,7 @@ def main():
             "frame_sha1": frame_sha1,
             "build_id": bid,
             "per_rank_ms": {"kernel": [round(x[0], 3) for x in per_rank],
-                            "gather": [round(x[1], 3) for x in per_rank]},
+                            "gather": [round(x[1], 3) if x[1] == x[1] else None for x in per_rank]},
         }
         ref_hash = n1_frame_hash(pmc_key)
         out["frame_sha1_n1"] = ref_hash

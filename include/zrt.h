@@ -44,7 +44,9 @@
 extern "C" {
 #endif
 
-#define ZRT_ABI_VERSION 1
+/* 2: zrt_stats gained sampling_loop (its size changed) and zrt_build_id was added;
+ * a client built against version 1 must not pass its smaller zrt_stats. */
+#define ZRT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 enum {

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_sizes():
     lib = _ffi.load()
-    assert lib.zrt_abi_version() == 1
+    assert lib.zrt_abi_version() == 2 == _ffi.ABI_VERSION
     assert b"gfx950" in lib.zrt_build_info()
     assert C.sizeof(_ffi.Prim) == 60 and C.sizeof(_ffi.Camera) == 48
     assert C.sizeof(_ffi.Params) == 64 and C.sizeof(_ffi.BvhNode) == 32
@@ -136,6 +136,27 @@ def test_param_validation_without_device(scenes):
             with pytest.raises(z.ZrtError) as e:
                 call()
             assert e.value.code == _ffi.ZRT_E_NODEVICE
+
+
+def test_tree_layout_mismatch_is_refused(scenes, monkeypatch):
+    """a wide tree whose encoding is not the one the kernels
+    decode (accel_build.hpp kLayout*, render.hip kKernelLayout) is refused with
+    ZRT_E_UNSUPPORTED before anything is launched - here on CPU, where the check
+    runs before the device check.  (The kernels repeat the check on the device:
+    kErrLayout.)"""
+    s = scenes(2)
+    monkeypatch.setenv("ZRT_DEBUG_TREE_LAYOUT", "1")  # flips the sphere-slot bit of the recorded layout
+    for call in (lambda: z.render(s, s.camera, z.RenderParams(8, 8, 1, 5)),
+                 lambda: z.RenderContext(s, z.RenderParams(8, 8, 1, 5))):
+        with pytest.raises(z.ZrtError) as e:
+            call()
+        assert e.value.code == _ffi.ZRT_E_UNSUPPORTED and "layout" in str(e.value)
+    monkeypatch.delenv("ZRT_DEBUG_TREE_LAYOUT")
+    import torch
+    if not torch.cuda.is_available():  # the matching layout passes on to the device check
+        with pytest.raises(z.ZrtError) as e:
+            z.render(s, s.camera, z.RenderParams(8, 8, 1, 5))
+        assert e.value.code == _ffi.ZRT_E_NODEVICE
 
 
 def test_oracle_counters_readme_rays_per_sample(scenes):

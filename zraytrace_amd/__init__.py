@@ -35,7 +35,7 @@ def lib():
 
 # csrc/Makefile ID_SRC, in its order, then include/zrt.h
 _ID_SRC = ("render.hip", "bvh_gpu.hip", "accel_build.cpp", "accel_build.hpp", "bvh_build.cpp", "bvh_build.hpp",
-           "device_math.hpp", "zrt.hpp")
+           "device_math.hpp", "zrt.hpp", "scene_io.cpp", "image_io.cpp", "cli.cpp")
 
 
 def build_id() -> str:

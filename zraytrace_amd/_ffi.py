@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZRT_LIB") or os.path.join(HERE, "libzrt.so")
 
 # ---- status / enums (zrt.h) --------------------------------------------------
+ABI_VERSION = 2  # ZRT_ABI_VERSION: the layouts below (zrt_stats gained sampling_loop in 2)
 ZRT_OK = 0
 ZRT_E_INVALID = -1
 ZRT_E_NOMEM = -2
@@ -209,6 +210,9 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
+    if path == os.path.join(HERE, "libzrt.so") and lib.zrt_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path} has ABI version {lib.zrt_abi_version()}, this binding expects {ABI_VERSION}: "
+                          "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
     if path == LIB_PATH:
         _lib = lib
     return lib

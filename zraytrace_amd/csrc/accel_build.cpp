@@ -173,6 +173,7 @@ void put4(float4v& q, int lane, float v) { q.v[lane] = v; }
 WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, float inflate, float sphere_grow,
                        bool mark_spheres) {
   WideBvh out;
+  out.layout = kLayoutVersion | (mark_spheres ? kLayoutSphereSlots | kLayoutSphereFirst : 0u);
   const size_t n = leaves.size();
   out.n_leaves = uint32_t(n);
   std::vector<Item> items(n);

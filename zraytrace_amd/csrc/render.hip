@@ -121,7 +121,12 @@ struct KArgs {
   float root_c[3], origin_bound;
   uint32_t check_origins;  // 0: every ray of the launch starts inside the bound (the camera does, checked
                            // on the host, and scattered rays start at hits), so ray_origin_ok is skipped
+  uint32_t layout;         // the wide tree's encoding (accel_build.hpp kLayout*): must equal kKernelLayout
 };
+
+// error_flag bits (zrt_ctx_sync / zrt_ctx_stats / zrt_render report them as ZRT_E_UNSUPPORTED)
+constexpr uint32_t kErrOverflow = 1u;  // a traversal stack deeper than it was sized for
+constexpr uint32_t kErrLayout = 2u;    // the wide tree's encoding is not the one this kernel decodes
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
@@ -729,7 +734,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
       }
       sp += 2;
     } else {
-      atomicOr(a.error_flag, 1u);
+      atomicOr(a.error_flag, kErrOverflow);
     }
   }
 }
@@ -780,7 +785,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
           if (sp < cap) stk[(sp++) * stride] = (StackT)far_idx;
-          else atomicOr(a.error_flag, 1u);  // too deep for the stack: the subtree is dropped (flagged)
+          else atomicOr(a.error_flag, kErrOverflow);  // too deep for the stack: the subtree is dropped (flagged)
           left = rfirst ? as_int(r0.w) : as_int(l0.w);
           right = rfirst ? as_int(r1.w) : as_int(l1.w);
           continue;
@@ -829,7 +834,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
           stk[(sp + 1) * stride] = (StackT)left;
           sp += 2;
         } else {
-          atomicOr(a.error_flag, 1u);
+          atomicOr(a.error_flag, kErrOverflow);
         }
       }
     }
@@ -900,6 +905,15 @@ __device__ __forceinline__ SlotT slot_interval(float nx, float ny, float nz, flo
 #ifndef ZRT_SPHERE_SLOTS
 #define ZRT_SPHERE_SLOTS 1  // A/B only: 0 culls sphere leaves like triangle leaves (not exact, DESIGN.md §3 "Spheres")
 #endif
+// The wide-tree encoding these kernels decode (accel_build.hpp kLayout*); the
+// host refuses any other before launching, and a kernel handed one anyway sets
+// kErrLayout and returns without reading the tree.
+constexpr uint32_t kKernelLayout = kLayoutVersion | (ZRT_SPHERE_SLOTS ? kLayoutSphereSlots | kLayoutSphereFirst : 0u);
+__device__ __forceinline__ bool layout_ok(const KArgs& a) {
+  if (a.layout == kKernelLayout) return true;  // (block-uniform: every thread returns together)
+  if (threadIdx.x == 0) atomicOr(a.error_flag, kErrLayout);
+  return false;
+}
 // The reference's loose test (aabb.zig:109-127) with t_max = +inf: every axis's
 // (post-swap) slab [n, f] reaches past t_min and is not empty.  max(n, t_min) /
 // min(f, +inf) as maxNum / minNum: a NaN bound constrains nothing, as math.max /
@@ -1241,7 +1255,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     const uint32_t nsp = sp + n - 1;
     // the host sizes cap = the tree's deepest stack + 3, so this never fires
     // unless the stack was sized too small: then entries would be lost
-    if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, 1u);
+    if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, kErrOverflow);
     sp = min(nsp, cap - 3);
     next = r0;
   } else if (sp != 0) {
@@ -1678,6 +1692,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
   lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  if (MODE == 3 && !layout_ok(a)) return;
   if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
@@ -1909,6 +1924,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
   lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  if (!layout_ok(a)) return;
   if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
@@ -2132,6 +2148,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the lane's traversal stack column
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  if (!layout_ok(a)) return;
   if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
@@ -2431,6 +2448,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
+  if (MODE == 3 && !layout_ok(a)) return;
   if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
   if (gl >= n) return;
@@ -2779,6 +2797,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint32_t> leaf_of_slot;
   zrt::DevBuf<uint8_t> ref_sph;
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;
+  uint32_t layout = 0;  // the wide tree's encoding (KArgs::layout)
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
@@ -2835,6 +2854,7 @@ struct HostScene {
   float scene_extent = 0.0f;  // KArgs::scene_extent
   float tri_c[3] = {0.0f, 0.0f, 0.0f}, tri_h[3] = {0.0f, 0.0f, 0.0f};  // KArgs::tri_c / tri_h
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;  // KArgs::root_c / origin_bound
+  uint32_t layout = 0;           // KArgs::layout: the wide tree's encoding
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
@@ -2941,14 +2961,34 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       c->ref_sph[i] = f;
       any_sphere = any_sphere || f;
     }
+    // The region the bound is sized over: the root box united with every sphere's
+    // centre -+ |radius|.  A negative radius (the reference scenes use them) makes
+    // sphere.zig:25's box inverted, so the root box alone need not cover that
+    // sphere's surface.
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = bvh.nodes[0].mn[k];
+      hi[k] = bvh.nodes[0].mx[k];
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      const zrt_prim& p = s->prims[i];
+      if (p.kind != ZRT_PRIM_SPHERE) continue;
+      const float r = std::fabs(p.radius), cc[3] = {p.center.x, p.center.y, p.center.z};
+      for (int k = 0; k < 3; ++k) {  // (rounded outward: the f32 box contains the exact one)
+        lo[k] = std::min(lo[k], std::nextafter(cc[k] - r, -HUGE_VALF));
+        hi[k] = std::max(hi[k], std::nextafter(cc[k] + r, HUGE_VALF));
+      }
+    }
     float H = 0.0f;
     for (int k = 0; k < 3; ++k) {
-      const BuildNode& root = bvh.nodes[0];
-      c->root_c[k] = 0.5f * root.mn[k] + 0.5f * root.mx[k];
-      H = std::max(H, 0.5f * (root.mx[k] - root.mn[k]));
+      c->root_c[k] = 0.5f * lo[k] + 0.5f * hi[k];
+      H = std::max(H, std::max(hi[k] - c->root_c[k], c->root_c[k] - lo[k]));
     }
     if (!(H < 0x1p100f)) H = 0x1p100f;  // NaN / huge extents: every origin fails ray_origin_ok's bound
-    c->origin_bound = 2.0f * H;
+    // Only sphere slots depend on where a ray starts (their growth is sized for
+    // origins within 2 H); the triangle margins do not, so a scene without spheres
+    // accepts every origin (a distant camera no longer replays every ray)
+    c->origin_bound = any_sphere ? 2.0f * H : HUGE_VALF;
     const float sphere_grow = any_sphere ? float(std::ldexp(std::sqrt(2.0), -9) * (3.0 * std::sqrt(3.0) + 1.0) * double(H)) : 0.0f;
     const double tw = now_ms();
     const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
@@ -2977,6 +3017,13 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
     c->n_top = wide.n_top;
+    c->layout = wide.layout;
+    if (const char* e = std::getenv("ZRT_DEBUG_TREE_LAYOUT"))  // tests: a tree another kernel would have to decode
+      c->layout ^= uint32_t(std::strtoul(e, nullptr, 0));
+    if (c->layout != kKernelLayout)
+      throw Error(ZRT_E_UNSUPPORTED, "the wide tree's layout (" + std::to_string(c->layout) +
+                                         ") is not the one this library's kernels decode (" +
+                                         std::to_string(kKernelLayout) + "): accel_build and render.hip disagree");
   } else {
     for (uint32_t i = 0; i < n; ++i) slot_to_prim.push_back(i);
   }
@@ -3128,6 +3175,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->ref_sph.upload(h.ref_sph);
   for (int k = 0; k < 3; ++k) c->root_c[k] = h.root_c[k];
   c->origin_bound = h.origin_bound;
+  c->layout = h.layout;
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -3336,6 +3384,8 @@ int hip_fail(const HipError& e) {
   }
 
 constexpr const char* kOverflowMsg = "BVH traversal stack overflow (tree deeper than the stack was sized for)";
+constexpr const char* kLayoutMsg = "the kernel refused the wide tree: its layout is not the one the kernel decodes";
+const char* device_error_msg(unsigned long long flag) { return (flag & kErrLayout) ? kLayoutMsg : kOverflowMsg; }
 
 // The device error flag of the context's last launch, copied to pinned host
 // memory behind ev_done.  wait: block until the launch is done and report its
@@ -3350,7 +3400,7 @@ int launch_status(zrt_ctx* c, bool wait) {
   }
   if (*c->err_host == 0) return ZRT_OK;
   c->err_reported = true;
-  return fail(ZRT_E_UNSUPPORTED, kOverflowMsg);
+  return fail(ZRT_E_UNSUPPORTED, device_error_msg(*c->err_host));
 }
 
 // RCCL for zrt_render_multi, opened on first use so that single-GPU callers do
@@ -3496,13 +3546,18 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
   int rc = zrt::validate_scene(scene);
   if (rc) return rc;
   if (!params) return fail(ZRT_E_INVALID, "params is null");
-  rc = zrt::check_device(int(params->device));
-  if (rc) return rc;
   try {
-    // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces
+    // raytrace.zig:124-133: BVH iff requested and more than 10 surfaces.  The
+    // scene is flattened before the device is checked, so a tree whose layout
+    // the kernels do not decode is refused on any machine (flatten_scene); the
+    // GPU builds the reference BVH only when one is visible
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
+    int n_dev = 0;
+    const bool have_dev = hipGetDeviceCount(&n_dev) == hipSuccess && int(params->device) < n_dev;
     zrt::HostScene h;
-    zrt::flatten_scene(&h, scene, use_bvh, int(params->device));
+    zrt::flatten_scene(&h, scene, use_bvh, have_dev ? int(params->device) : -1);
+    rc = zrt::check_device(int(params->device));
+    if (rc) return rc;
     *out = zrt::ctx_on_device(h, int(params->device)).release();
     return ZRT_OK;
   } catch (const zrt::HipError& e) {
@@ -3656,6 +3711,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.ref_sph = c->ref_sph.p;
     for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
     a.origin_bound = c->origin_bound;
+    a.layout = c->layout;
     {  // the camera inside the bound: so is every ray of the launch (scattered rays start at hits)
       const float m = std::max({std::fabs(a.org[0] - a.root_c[0]), std::fabs(a.org[1] - a.root_c[1]),
                                 std::fabs(a.org[2] - a.root_c[2])});
@@ -4072,10 +4128,14 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
     zrt_stats sum;
     std::memset(&sum, 0, sizeof(sum));
     int device_rc = ZRT_OK;
+    std::string device_msg;
     for (uint32_t r = 0; r < n; ++r) {
       zrt_stats s;
       rc = zrt_ctx_stats(m->ctx[r].get(), &s);  // waits for rank r's launch
-      if (rc == ZRT_E_UNSUPPORTED) device_rc = rc;  // device error: finish the frame (NaN tiles), then report it
+      if (rc == ZRT_E_UNSUPPORTED) {  // device error: finish the frame (NaN tiles), then report it
+        device_rc = rc;
+        device_msg = zrt_last_error();
+      }
       else if (rc) return rc;
       if (r == 0) {
         sum = s;
@@ -4135,7 +4195,7 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
     HIPCHK(hipMemcpy(out_rgb, m->frame.p, sizeof(float) * frame_n, hipMemcpyDeviceToHost));
     sum.n_gpus = m->n_distinct;
     if (stats) *stats = sum;
-    if (device_rc) return fail(device_rc, zrt::kOverflowMsg);
+    if (device_rc) return fail(device_rc, device_msg);
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
@@ -4225,6 +4285,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
     a.origin_bound = c->origin_bound;
     a.check_origins = 1;  // arbitrary ray origins
+    a.layout = c->layout;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
@@ -4249,7 +4310,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     HIPCHK(hipStreamSynchronize(c->stream));
     unsigned long long err = 0;
     HIPCHK(hipMemcpy(&err, c->scratch.p + zrt::kErrorSlot, sizeof(err), hipMemcpyDeviceToHost));
-    if (err) return fail(ZRT_E_UNSUPPORTED, "BVH traversal stack overflow (tree deeper than sized)");
+    if (err) return fail(ZRT_E_UNSUPPORTED, zrt::device_error_msg(err));
     std::vector<int32_t> slot(n_rays);
     HIPCHK(hipMemcpy(out_t, d_t.p, sizeof(float) * n_rays, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(slot.data(), d_slot.p, sizeof(int32_t) * n_rays, hipMemcpyDeviceToHost));

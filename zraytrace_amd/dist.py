@@ -97,10 +97,12 @@ class TileFrame:
         self.gather_ms = []  # per step: the gather (+ assemble on rank 0), HIP events on self.stream
         self._ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
 
-    def step(self, params=None) -> float:
+    def step(self, params=None, record: bool = None) -> float:
         """One frame; returns the render launch's kernel time in ms (HIP events
         on the launch stream).  `params` overrides the render params (e.g. the
-        diagnostic flag) for this step."""
+        diagnostic flag) for this step.  The gather (+ assemble) time is appended
+        to gather_ms when `record` is true - by default for steps with the
+        frame's own params, so an extra diagnostic launch does not count."""
         import torch
         p = params or self.params
         with torch.cuda.stream(self.stream):
@@ -112,7 +114,7 @@ class TileFrame:
                 self.ctx.assemble_padded(self.p0, g.data_ptr(), max(1, self.max_tiles), self.frame.data_ptr(),
                                          self.stream.cuda_stream)
             self._ev[1].record(self.stream)
-        if params is None:
+        if record or (record is None and params is None):
             self._ev[1].synchronize()
             self.gather_ms.append(self._ev[0].elapsed_time(self._ev[1]))
         return kms
