@@ -390,7 +390,8 @@ def main():
         # SIMD efficiency of the loop (STATS launch, zrt_ctx_debug_counters slots 4 / 21-23):
         # lane node visits / (64 x the wave's traversal trips), and the lanes that ran a
         # rayColor step / (64 x loop iterations that ran one)
-        loops = {0: "list", 1: "binary", 2: "reference", 3: "lockstep", 4: "wavefront", 5: "path pool"}
+        loops = {0: "list", 1: "binary", 2: "reference", 3: "lockstep", 4: "wavefront", 5: "path pool",
+                 6: "list, per-lane items"}
         # (an A/B variant built before zrt_stats.sampling_loop existed leaves it zero: "unknown", not "list")
         simd = {"sampling_loop": loops.get(int(st.get("sampling_loop", -1)), "unknown") if bid != "unknown"
                 else "unknown"}

@@ -222,7 +222,7 @@ typedef struct zrt_stats {
   uint64_t box_excess_hits;
   /* the sampling loop of the last launch: 0 surface list, 1
    * binary / 2 reference BVH traversal, FAST traversal: 3 lockstep, 4 wavefront,
-   * 5 path pool */
+   * 5 path pool; 6 surface list with per-lane work items */
   uint32_t sampling_loop;
 } zrt_stats;
 

@@ -162,6 +162,30 @@ def test_render_loops_bit_exact(scenes, case, loop, monkeypatch):
     np.testing.assert_array_equal(rows, rrows)
 
 
+@pytest.mark.parametrize("lanes", ["items", "wave"])
+@pytest.mark.parametrize("w,h,spp,chunk", [(40, 40, 24, 7), (45, 30, 9, 4)])
+def test_list_loops_bit_exact(scenes, lanes, w, h, spp, chunk, monkeypatch):
+    """The surface-list loops on scene 1 (seven spheres, glass and metal, depth 30:
+    config C2's scene): per-lane work items (render_loop_list, the default) and
+    the wave-unit loop (render_loop MODE 0, ZRT_LIST_LANES=0), with chunks that
+    split the samples and a ragged frame: images, counters and per-scanline
+    counters equal the oracle's."""
+    monkeypatch.setenv("ZRT_LIST_LANES", "1" if lanes == "items" else "0")
+    s = scenes(1)
+    p = z.RenderParams(w, h, spp, 30, sample_chunk=chunk)
+    gpu, gs, rows = z.render_progress(s, s.camera, p)
+    ref, rs, rrows = O.render_scanlines(s.view, s.camera, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+    np.testing.assert_array_equal(rows, rrows)
+    assert gs["sampling_loop"] == (6 if lanes == "items" else 0)
+    img2, gs2 = z.render(s, s.camera, p)  # without the scanline flag: counters from the wave sums
+    assert_bit_exact(img2, ref)
+    for k in COUNTERS:
+        assert gs2[k] == rs[k], k
+
+
 def test_c5_substitute_bit_exact(scenes):
     """Scene 6, the stated C5 substitute: 1.6 M subdivided teapot triangles
     (reference BVH 1 894 803 nodes, depth 39) with image-textured lambertians on both surfaces, so the

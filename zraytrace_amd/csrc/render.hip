@@ -122,6 +122,7 @@ struct KArgs {
   uint32_t check_origins;  // 0: every ray of the launch starts inside the bound (the camera does, checked
                            // on the host, and scattered rays start at hits), so ray_origin_ok is skipped
   uint32_t layout;         // the wide tree's encoding (accel_build.hpp kLayout*): must equal kKernelLayout
+  float graze_m;           // the grazing margins' coefficient (RayT::gm; DESIGN.md §3 "Grazing rays")
 };
 
 // error_flag bits (zrt_ctx_sync / zrt_ctx_stats / zrt_render report them as ZRT_E_UNSUPPORTED)
@@ -344,6 +345,9 @@ struct RayT {
   // triangle.zig:61 that passes det >= 1e-6 lies in dev::rcp_core's range; a
   // wave-uniform value (from KArgs), so the choice below is a scalar branch
   uint32_t rcp_det;
+  // the scene's grazing-margin coefficient (KArgs::graze_m, 2^-18 by default):
+  // wave-uniform, so it stays in an SGPR
+  float gm;
 };
 
 // A computed primitive hit lies outside its own box: a triangle's by a few ulps
@@ -384,10 +388,10 @@ __device__ __forceinline__ float ray_m(const RayT& r) {  // max_k |1/d_k|
   return __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ix), __builtin_fabsf(r.iy)), __builtin_fabsf(r.iz));
 }
 // relative margin of every narrowed cull: 1 + 2^-16 + 2^-18 m
-__device__ __forceinline__ float ray_rel(float m) { return ZRT_REL_M ? 1.0000153f + 0x1p-18f * m : 1.0000153f; }
+__device__ __forceinline__ float ray_rel(const RayT& r, float m) { return ZRT_REL_M ? 1.0000153f + r.gm * m : 1.0000153f; }
 // the reference boxes' slack: 2^-18 x the triangles' largest |coordinate| x m
-__device__ __forceinline__ float ray_slack(float extent, float m) {
-  return ZRT_LEAF_SLACK ? __builtin_fmaxf(extent, 0x1p-100f) * 0x1p-18f * m : 0.0f;
+__device__ __forceinline__ float ray_slack(const RayT& r, float extent, float m) {
+  return ZRT_LEAF_SLACK ? __builtin_fmaxf(extent, 0x1p-100f) * r.gm * m : 0.0f;
 }
 
 // Nearly axis-parallel rays (DESIGN.md §3 "Per-axis margins").  The margins
@@ -415,7 +419,7 @@ constexpr float kPaxisM = float(1u << ZRT_PAXIS_LOG2M);
 __device__ __forceinline__ float paxis_grow(const KArgs& a, const RayT& r) {
   const float T = (__builtin_fabsf(r.ox - a.tri_c[0]) + a.tri_h[0]) + (__builtin_fabsf(r.oy - a.tri_c[1]) + a.tri_h[1]) +
                   (__builtin_fabsf(r.oz - a.tri_c[2]) + a.tri_h[2]);  // >= the L2 distance to any corner
-  return (T + __builtin_fmaxf(a.scene_extent, 0x1p-100f)) * 0x1.0001p-18f;  // (rounding of T: the extra 2^-16)
+  return (T + __builtin_fmaxf(a.scene_extent, 0x1p-100f)) * (r.gm * 1.0000153f);  // (rounding of T: the extra 2^-16)
 }
 // the per-axis term in t, finite (an infinite 1/d_k keeps the slab's exact +-inf:
 // the reference's own test then rejects every leaf off the plane)
@@ -447,7 +451,7 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && (!narrow || !(en > __builtin_fmaf(ex, ray_rel(ray_m(r)), slack)));
+    ok = ok && (!narrow || !(en > __builtin_fmaf(ex, ray_rel(r, ray_m(r)), slack)));
     *entry = en;
   }
   return ok;
@@ -705,7 +709,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
                                               float& best_t, int& best, bool narrow = true) {
   const uint32_t rows = a.lds_rows, cap = a.ref_stack;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
-  const float slack = ray_slack(a.scene_extent, ray_m(r));
+  const float slack = ray_slack(r, a.scene_extent, ray_m(r));
   best_t = __builtin_inff();
   best = -1;
   uint32_t c_tri = 0, c_sph = 0;
@@ -760,7 +764,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
   uint32_t sp = 0;
   const uint32_t cap = a.stack_depth;
   if (FAST) {
-    const float slack = ray_slack(a.scene_extent, ray_m(r));
+    const float slack = ray_slack(r, a.scene_extent, ray_m(r));
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
@@ -865,7 +869,7 @@ __device__ __forceinline__ float wide_slot(float mnx, float mny, float mnz, floa
   const float cn = __builtin_fmaxf(c0, t_min), cx = __builtin_fminf(c1, tb);
   const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
   const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-  bool ok = !(en > ex * ray_rel(ray_m(r)));
+  bool ok = !(en > ex * ray_rel(r, ray_m(r)));
   if (leaf) ok = ok && (ax > an) && (bx > bn) && (cx > cn);  // !(tmax <= tmin) per axis
   return ok ? en : __builtin_inff();
 }
@@ -955,7 +959,7 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
       __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(f[px]), __builtin_fabsf(f[qx])),
                       __builtin_fmaxf(__builtin_fabsf(f[py]), __builtin_fabsf(f[qy]))),
       __builtin_fmaxf(__builtin_fabsf(f[pz]), __builtin_fabsf(f[qz])));
-  const float g = cl * 0x1p-18f;
+  const float g = cl * r.gm;
   const float gx = g * __builtin_fabsf(r.ix), gy = g * __builtin_fabsf(r.iy), gz = g * __builtin_fabsf(r.iz);
   const float tl = tb + __builtin_fmaxf(__builtin_fmaxf(gx, gy), gz);
   const bool loose = (__builtin_fminf(fx, tl) > __builtin_fmaxf(nx, t_min)) &&
@@ -964,7 +968,7 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   // the narrowed test of the box grown by g (NaN bounds constrain nothing)
   const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
   const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
-  return loose && !(en > ex * ray_rel(ray_m(r)));
+  return loose && !(en > ex * ray_rel(r, ray_m(r)));
 }
 
 // static_ok of leaf slot k, its slab distances recomputed from the node in memory
@@ -1121,7 +1125,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool sx = v.sx, sy = v.sy, sz = v.sz;
   int r0 = as_int(w.ra.x), r1 = as_int(w.ra.y), r2 = as_int(w.ra.z), r3 = as_int(w.ra.w);
   const float tb = __builtin_fabsf(best_t) * kOpen;
-  const float m = ray_m(r), rel = ray_rel(m), slk = ray_slack(a.scene_extent, m);
+  const float m = ray_m(r), rel = ray_rel(r, m), slk = ray_slack(r, a.scene_extent, m);
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
@@ -1809,6 +1813,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       r.ox = o.x; r.oy = o.y; r.oz = o.z;
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
       r.rcp_det = a.tri_rcp_fast;
+      r.gm = a.graze_m;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
             float best_t = __builtin_inff();
       int best = -1;
@@ -1948,6 +1953,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   // the ray in flight and its suspended traversal
   RayT r{};
   r.rcp_det = a.tri_rcp_fast;
+  r.gm = a.graze_m;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2188,6 +2194,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   uint32_t cp = 0;  // its path (0 .. kPoolPaths-1 of this wave)
   RayT r{};
   r.rcp_det = a.tri_rcp_fast;
+  r.gm = a.graze_m;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2401,8 +2408,172 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The surface-list loop with per-lane work items (MODE 6; raytrace.zig:71-81
+// without a BVH, config C2).  Every ray of a list scene costs the same - all
+// n_list surfaces, read through the scalar cache - so the coherence that makes
+// the lockstep loop win on a BVH buys nothing here, while its waits cost most
+// of the lanes: a wave that steps sample by sample waits for its longest path
+// (C2: 2.14 rays per sample, glass paths up to depth 30; VALU lane utilisation
+// 0.31).  Here a work item is one (pixel, chunk) - the 64 items of a unit are
+// the 64 pixels of its tile - and each lane runs its own item's samples in
+// order and takes the next item as soon as it is done: the lanes of a wave
+// needing one share one atomic (ballot + mbcnt rank).  The chunk's sum is the
+// same sequential sum in the same slot, so images are bit-identical to the
+// other loops'.
+// ---------------------------------------------------------------------------
+template <int PRNG, bool STATS>
+__device__ __forceinline__ void render_loop_list(const KArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  const DevMaterial* mats = a.mats;
+  if (a.mats_in_lds) {  // block-uniform
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) float4 cfloat4;  // the list is wave-uniform: scalar loads
+  cfloat4* cprims = (cfloat4*)a.prims;
+  cfloat4* cshade = (cfloat4*)a.shade;
+#else
+  const float4* cprims = a.prims;
+  const float4* cshade = a.shade;
+#endif
+  const int lane = (int)__lane_id();
+  const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t total_items = a.total_work * 64u;  // < 2^32 (host check on tiles x 64 x chunks)
+
+  bool has = false, in_sample = false;  // this lane holds an item / one of its samples is under way
+  bool exhausted = false;               // wave-uniform: every item has been handed out
+  uint32_t sample = 0, s_end = 0, slot = 0, px = 0, py = 0;
+  float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
+  V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+  uint32_t depth_left = 0;
+  Rng<PRNG> rng;
+  rng.init(0);
+  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_tri = 0, c_sph = 0, c_shade = 0, c_tex = 0;
+  uint32_t c_loops = 0, c_lsteps = 0;
+  Coh coh;  // STATS
+  for (;;) {
+    // ---- refill: the lanes without an item take the next ones, one atomic per wave
+    const uint64_t need = __ballot(!has);
+    if (need != 0ull && !exhausted) {
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(need);
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(a.work_counter, cnt);
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (base >= total_items || total_items - base <= cnt) exhausted = true;
+      if (!has) {
+        const uint32_t rank =
+            (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const uint32_t item = base + rank;  // (base + rank wraps only past total_items: no item then)
+        if (base < total_items && item < total_items) {
+          const uint32_t u = item >> 6, p = item & 63u;
+          const uint32_t ord = u / a.n_chunks, g = u - ord * a.n_chunks;
+          const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;
+          const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
+          px = (t % a.tiles_x) * 8u + (p & 7u);
+          py = (t / a.tiles_x) * 8u + (p >> 3);
+          if (px < a.xbound && py < a.height) {  // off-frame pixels: nothing (finalize writes black)
+            has = true;
+            in_sample = false;
+            sample = g * a.chunk;
+            s_end = min(sample + a.chunk, a.spp);
+            slot = g * a.n_slots + lt * 64u + p;
+            acc_r = acc_g = acc_b = 0.0f;
+          }
+        }
+      }
+    }
+    if (__ballot(has) == 0ull) {
+      if (exhausted) break;
+      continue;  // (every lane drew an off-frame pixel)
+    }
+    if (STATS) {
+      c_loops += lane == 0 ? 1u : 0u;
+      c_lsteps += has ? 1u : 0u;
+    }
+    if (!has) continue;
+    // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
+    if (!in_sample) {
+      const uint64_t offset = (uint64_t)py * a.width + px;
+      rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
+      const float u = dev::div_known((float)px + rand_float(rng) - 0.5f, a.f_width, a.inv_width);
+      const float v = dev::div_known((float)py + rand_float(rng) - 0.5f, a.f_height, a.inv_height);
+      o = mk(a.org[0], a.org[1], a.org[2]);
+      d = unit(sub(add(add(mk(a.llc[0], a.llc[1], a.llc[2]), scale(mk(a.hor[0], a.hor[1], a.hor[2]), u)),
+                       scale(mk(a.ver[0], a.ver[1], a.ver[2]), v)),
+                   o));
+      depth_left = a.max_depth;
+      in_sample = true;
+    }
+    // ---- one rayColor step (raytrace.zig:62-100)
+    bool path_end = false, sky = false;
+    V3 L = mk(0.0f, 0.0f, 0.0f);
+    const uint32_t dh0 = c_depth, rf0 = c_refl, bg0 = c_bg;
+    if (depth_left == 0) {
+      ++c_depth;
+      path_end = true;
+    } else {
+      if (STATS) ++c_rays;
+      RayT r;
+      r.ox = o.x; r.oy = o.y; r.oz = o.z;
+      r.dx = d.x; r.dy = d.y; r.dz = d.z;
+      r.rcp_det = a.tri_rcp_fast;
+      r.gm = a.graze_m;
+      inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
+      float best_t = __builtin_inff();
+      int best = -1;
+      for (uint32_t i = 0; i < a.n_list; ++i) {  // surfaces in list order, t_max shrinking
+        const uint32_t tag = __float_as_uint(cshade[i].w);
+        if (tag >> 31) {
+          if (STATS) ++c_tri;
+          tri_test_v<false>(cprims[3 * i], cprims[3 * i + 1], cprims[3 * i + 2], (int)i, r, best_t, best);
+        } else {
+          if (STATS) ++c_sph;
+          sphere_test<false>(cprims[3 * i], (int)i, r, best_t, best);
+        }
+      }
+      shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
+                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
+    }
+    if (a.scanlines) {  // this lane's item is one pixel: its events go to its row (raytrace.zig:184)
+      scanline_add(a, py, 0, c_depth - dh0);
+      scanline_add(a, py, 1, c_refl - rf0);
+      scanline_add(a, py, 2, c_bg - bg0);
+    }
+    if (path_end) {
+      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
+      acc_r += col.x;
+      acc_g += col.y;
+      acc_b += col.z;
+      in_sample = false;
+      if (++sample == s_end) {  // the chunk's sequential sum, in its [chunk][pixel slot] place
+        a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
+        has = false;
+      }
+    }
+  }
+  if (!a.scanlines) {  // (with ZRT_FLAG_SCANLINES they went to the frame rows, whose sums are the totals)
+    wave_add_u64(&a.counters[kDepthHits], c_depth);
+    wave_add_u64(&a.counters[kReflections], c_refl);
+    wave_add_u64(&a.counters[kBackground], c_bg);
+  }
+  if (STATS) {
+    wave_add_u64(&a.counters[kRays], c_rays);
+    wave_add_u64(&a.counters[kTriTests], c_tri);
+    wave_add_u64(&a.counters[kSphereTests], c_sph);
+    wave_add_u64(&a.counters[kShades], c_shade);
+    wave_add_u64(&a.counters[kTexels], c_tex);
+    wave_add_u64(&a.counters[kLoopTrips], c_loops);
+    wave_add_u64(&a.counters[kLaneSteps], c_lsteps);
+    coh.flush(a.counters);
+  }
+}
+
 #ifndef ZRT_ATT_ROWS_LIST
-#define ZRT_ATT_ROWS_LIST 8  // list loop (MODE 0): attenuation rows kept in LDS (as many as its 6-block share holds)
+#define ZRT_ATT_ROWS_LIST 8  // list loops (MODE 0 / 6): attenuation rows kept in LDS (as many as their 6-block share holds)
 #endif
 #ifndef ZRT_ATT_ROWS_WF
 #define ZRT_ATT_ROWS_WF 4  // wavefront loop: attenuation rows kept in LDS (A/B: 2 = the lockstep kernel's)
@@ -2422,10 +2593,11 @@ template <int MODE, int PRNG, bool STATS, class StackT>
 __global__ void __launch_bounds__(kBlock, MODE == 5   ? ZRT_WAVES_POOL
                                           : MODE == 4 ? ZRT_WAVES_WF
                                           : MODE == 3 ? ZRT_WAVES_WIDE
-                                          : MODE == 0 ? ZRT_WAVES_LIST
+                                          : MODE == 0 || MODE == 6 ? ZRT_WAVES_LIST
                                                       : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
-  if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT>(a);
+  if constexpr (MODE == 6) render_loop_list<PRNG, STATS>(a);
+  else if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT>(a);
   else if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
   else render_loop<MODE, PRNG, STATS, StackT>(a);
 }
@@ -2458,6 +2630,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   r.ox = q[0]; r.oy = q[1]; r.oz = q[2];
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
   r.rcp_det = a.tri_rcp_fast;
+  r.gm = a.graze_m;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
     float best_t = __builtin_inff();
   int best = -1;
@@ -2798,6 +2971,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint8_t> ref_sph;
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;
   uint32_t layout = 0;  // the wide tree's encoding (KArgs::layout)
+  float graze_m = 0x1p-18f;  // KArgs::graze_m
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
@@ -2855,6 +3029,7 @@ struct HostScene {
   float tri_c[3] = {0.0f, 0.0f, 0.0f}, tri_h[3] = {0.0f, 0.0f, 0.0f};  // KArgs::tri_c / tri_h
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;  // KArgs::root_c / origin_bound
   uint32_t layout = 0;           // KArgs::layout: the wide tree's encoding
+  float graze_m = 0x1p-18f;      // KArgs::graze_m (the inner boxes are grown by half of it)
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
@@ -2872,6 +3047,13 @@ constexpr uint32_t kDeviceBvhMin = 1u << 16;
 bool device_bvh(uint32_t n) {
   if (const char* e = std::getenv("ZRT_BVH_DEVICE")) return std::atoi(e) != 0;
   return n >= kDeviceBvhMin;
+}
+
+// The grazing margins' coefficient (DESIGN.md §3 "Grazing rays"): 2^-18;
+// ZRT_GRAZE_M overrides it (A/B of larger margins)
+float graze_margin() {
+  if (const char* e = std::getenv("ZRT_GRAZE_M")) return std::max(0x1p-18f, float(std::atof(e)));
+  return 0x1p-18f;
 }
 
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
@@ -2991,7 +3173,8 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     c->origin_bound = any_sphere ? 2.0f * H : HUGE_VALF;
     const float sphere_grow = any_sphere ? float(std::ldexp(std::sqrt(2.0), -9) * (3.0 * std::sqrt(3.0) + 1.0) * double(H)) : 0.0f;
     const double tw = now_ms();
-    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0x1p-19f : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
+    c->graze_m = graze_margin();
+    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0.5f * c->graze_m : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
                                           ZRT_SPHERE_SLOTS != 0);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
@@ -3176,6 +3359,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   for (int k = 0; k < 3; ++k) c->root_c[k] = h.root_c[k];
   c->origin_bound = h.origin_bound;
   c->layout = h.layout;
+  c->graze_m = h.graze_m;
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -3227,6 +3411,14 @@ bool use_pool(const zrt_ctx* c, bool stk16) {
   (void)c;
   return !stk16;
 }
+// The list loop with per-lane work items (render_loop_list, MODE 6) for scenes
+// without a BVH; ZRT_LIST_LANES=0 forces the wave-unit loop (render_loop MODE 0).
+// C2: 34.1 (MODE 0, lanes in per-sample lockstep) -> 45.4 (MODE 0, free lanes
+// within a unit) -> MODE 6.
+bool use_list_lanes() {
+  if (const char* e = std::getenv("ZRT_LIST_LANES")) return std::atoi(e) != 0;
+  return true;
+}
 // LDS of the path-pool loop's rays, hits and queues per block (render_loop_pool)
 constexpr size_t kPoolLdsBytes = ((8 * sizeof(float) + 1) * kBlockPaths + 15) & ~size_t(15);
 
@@ -3238,6 +3430,7 @@ void* kernel_ptr() {
 template <int PRNG, bool STATS>
 void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 0) return kernel_ptr<0, PRNG, STATS, uint16_t>();  // list mode: no stack
+  if (mode == 6) return kernel_ptr<6, PRNG, STATS, uint16_t>();  // list mode, per-lane work items
   if (mode == 1) return stk16 ? kernel_ptr<1, PRNG, STATS, uint16_t>() : kernel_ptr<1, PRNG, STATS, uint32_t>();
   if (mode == 3) return stk16 ? kernel_ptr<3, PRNG, STATS, uint16_t>() : kernel_ptr<3, PRNG, STATS, uint32_t>();
   if (mode == 4) return stk16 ? kernel_ptr<4, PRNG, STATS, uint16_t>() : kernel_ptr<4, PRNG, STATS, uint32_t>();
@@ -3631,7 +3824,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * zrt::kOctCopies : 0;
       if (size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) + top + zrt::kPoolLdsBytes > budget) stk16 = false;
     }
-    void* kfn = zrt::select_kernel(pool ? 5 : wf ? 4 : mode, p->prng, diag, stk16);
+    const bool list_lanes = mode == 0 && zrt::use_list_lanes();
+    const int kmode = pool ? 5 : wf ? 4 : list_lanes ? 6 : mode;
+    void* kfn = zrt::select_kernel(kmode, p->prng, diag, stk16);
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
@@ -3646,7 +3841,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint32_t chunk = p->sample_chunk ? p->sample_chunk : ZRT_DEFAULT_SAMPLE_CHUNK;
     const uint32_t n_chunks = (p->samples_per_pixel + chunk - 1) / chunk;
     const uint64_t work64 = uint64_t(my_tiles) * n_chunks;  // units: (tile, chunk)
-    if (uint64_t(my_tiles) * 64u * n_chunks >= (1ull << 32))
+    if (uint64_t(my_tiles) * 64u * n_chunks >= (1ull << 32) - (1ull << 26))  // (+ one refill per lane of slack)
       return fail(ZRT_E_UNSUPPORTED, "more than 2^32 (pixel, chunk) work items");
     const uint32_t work = uint32_t(work64);
     // one wave per unit at the start; more waves than units would only idle
@@ -3712,6 +3907,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     for (int k = 0; k < 3; ++k) a.root_c[k] = c->root_c[k];
     a.origin_bound = c->origin_bound;
     a.layout = c->layout;
+    a.graze_m = c->graze_m;
     {  // the camera inside the bound: so is every ray of the launch (scattered rays start at hits)
       const float m = std::max({std::fabs(a.org[0] - a.root_c[0]), std::fabs(a.org[1] - a.root_c[1]),
                                 std::fabs(a.org[2] - a.root_c[2])});
@@ -3745,7 +3941,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_chunks = n_chunks;
     a.wf_thresh = 48;  // shade once 3/4 of the unit's active lanes are ready (C5: 32 -> 7.32, 48 -> 7.71, 56 -> 7.70 Gray/s)
     if (const char* e = std::getenv("ZRT_WF_THRESH")) a.wf_thresh = std::max(1, std::min(64, std::atoi(e)));
-    a.sync = ZRT_SYNC_SAMPLES;
+    // the lockstep interval: the BVH loops keep a wave's lanes on one sample (its
+    // camera rays coherent); the list loop gains nothing from that (every ray reads
+    // the same surfaces) and lets its lanes run through the unit's chunk
+    // (C2: 34.1 -> 45.4 Gray/s, profiles/r04/s1)
+    a.sync = mode == 0 ? chunk : ZRT_SYNC_SAMPLES;
     if (const char* e = std::getenv("ZRT_SYNC"))  // A/B: lockstep interval in samples (identical images)
       a.sync = std::max(1u, uint32_t(std::atoi(e)));
     a.n_slots = my_tiles * 64u;
@@ -3801,7 +4001,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_xbound = g.xbound;
     c->last_stats = diag;
     c->last_mode = mode;
-    c->last_loop = pool ? 5 : wf ? 4 : mode;
+    c->last_loop = kmode;
     c->launched = 1;
     return ZRT_OK;
   }
@@ -4286,6 +4486,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.origin_bound = c->origin_bound;
     a.check_origins = 1;  // arbitrary ray origins
     a.layout = c->layout;
+    a.graze_m = c->graze_m;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
