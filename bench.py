@@ -55,11 +55,11 @@ def algorithmic_bytes(st, n_work_units, n_pixels):
     per node record read (32 B binary/reference node; 128 B wide node, which
     also carries its leaf children's boxes), 48 B per triangle test, 16 B per sphere test,
     64 B per shaded hit (16 B shade record + 48 B material), 4 B (8-bit store) or 12 B (f32) per texel,
-    32 B per scatter (attenuation pushed + read back), 16 B per chunk sum
+    8 B per scatter (its 4-B attenuation code pushed + read back), 16 B per chunk sum
     written and read, 12 B per output pixel."""
     tri = st["prim_tests"] - st["sphere_tests"]
     return (st["node_bytes"] * st["node_visits"] + 48 * tri + 16 * st["sphere_tests"] + 64 * st["shade_fetches"]
-            + (st["texel_bytes"] or 12) * st["texel_fetches"] + 32 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
+            + (st["texel_bytes"] or 12) * st["texel_fetches"] + 8 * st["reflections"] + 32 * n_work_units + 12 * n_pixels)
 
 
 def pmc_entry(config, build_id):
@@ -371,7 +371,7 @@ def main():
         # counter kAttWrites of the diagnostic launch) and, on deep trees, the traversal
         # stack entries past the LDS rows (u32; kStackOvfWrites)
         dc = fr.ctx.debug_counters(32)
-        wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 16 * int(dc[28]),
+        wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 4 * int(dc[28]),  # 4-B att codes
               "stack_rows_B": 4 * int(dc[30])}  # FAST stack entries past the LDS rows (kStackOvfWrites)
         wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
         if pe and pe.get("write_size_kb"):

@@ -309,14 +309,16 @@ def test_device_bvh_failure_falls_back_to_host(scenes, monkeypatch):
     assert st["rays_processed"] == rst["rays_processed"]
 
 
-@pytest.mark.parametrize("scene_index,env,loop", [(1, {}, 0), (2, {}, 3), (2, {"ZRT_WF": "1", "ZRT_POOL": "0"}, 4),
+@pytest.mark.parametrize("scene_index,env,loop", [(1, {}, 6), (1, {"ZRT_LIST_LANES": "0"}, 0), (2, {}, 3),
+                                                  (2, {"ZRT_WF": "1", "ZRT_POOL": "0"}, 4),
                                                   (2, {"ZRT_POOL": "1"}, 5), (6, {}, 5)])
 def test_stats_report_the_sampling_loop(scenes, scene_index, env, loop, monkeypatch):
     """zrt_stats.sampling_loop names the loop the launch ran: the
-    surface list for the 7 spheres, the lockstep loop for the bunny, the path pool
+    surface list with per-lane work items for the 7 spheres (the wave-unit list
+    loop when ZRT_LIST_LANES=0), the lockstep loop for the bunny, the path pool
     for the 1.6 M-triangle C5 mesh (a tree past the 16-bit stack), and the loops
     ZRT_WF / ZRT_POOL force."""
-    for k in ("ZRT_WF", "ZRT_POOL"):
+    for k in ("ZRT_WF", "ZRT_POOL", "ZRT_LIST_LANES"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)

@@ -71,7 +71,7 @@ struct KArgs {
   const float* __restrict__ texels;    // f32 RGB images
   const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
   const float* __restrict__ lut255;      // k / 255.0f for k = 0..255 (png_image.zig:88)
-  float4* __restrict__ att;            // [max_depth][n_lanes]
+  uint32_t* __restrict__ att;          // [row - att_lds_rows][lane or path]: attenuation codes (att_code)
   float4* __restrict__ partial;        // [chunk][tile slot] chunk sums
   uint32_t* __restrict__ work_counter;
   uint32_t* __restrict__ unit_cost;         // probe: loop iterations a wave spent on each tile, else null
@@ -101,7 +101,7 @@ struct KArgs {
   // LDS beyond the stack rows (byte offsets into the block's dynamic LDS):
   uint32_t n_top;         // FAST: wide nodes 0 .. n_top-1 (the top levels) served from LDS
   uint32_t lds_top_off;   //   [copy][node][8] float4, copied in at kernel start
-  uint32_t lds_att_off;   // attenuation rows 0 .. att_lds_rows-1: [row][rgb][lane] f32
+  uint32_t lds_att_off;   // attenuation rows 0 .. att_lds_rows-1: [row][lane] u32 codes (att_code)
   uint32_t att_lds_rows;  //   (rows att_lds_rows.. in `att`, [row - att_lds_rows][lane])
   uint32_t lds_mat_off;   // the material table (n_mats DevMaterial), when mats_in_lds
   uint32_t n_mats, mats_in_lds;
@@ -892,6 +892,34 @@ __device__ __forceinline__ f2 slab2(float b0, float b1, float o, float inv) {
   return (f2){(b0 - o) * inv, (b1 - o) * inv};
 }
 
+// The same distances as fma(plane, 1/d, -o/d) (ZRT_FMA_SLABS): one rounding
+// after an exact product instead of (plane - o) * (1/d)'s two, 24 VALU fewer
+// per wide node.  With p = RN(o_k / d_k) such a distance lies within
+// 1.0002 u |p| + 3.0001 u |s| of the reference's RN(RN(plane - o) * (1/d))
+// (u = 2^-24); wide_iter's culls carry kFmaE2 * max_k |p_k| more slack for it
+// (both ends of an interval), the relative margin (>= 2^-16) covers the rest, and
+// each decision that must be the reference's own - a leaf's loose test, a sphere
+// slot's static test, the hazard entry - is taken from these values only when it
+// is certain by that margin (kFmaSure), else from the exact distances recomputed
+// from memory (loose_slot / static_ok_slot), as for intervals within the margin.
+// A ray with |1/d_k| >= 2^100 or |p_k| >= 2^120 (a direction component ~0) is
+// "degenerate": it culls everything here and is traced the reference's way
+// (wide_finish, ray_degenerate).
+#ifndef ZRT_FMA_SLABS
+#define ZRT_FMA_SLABS 1  // 0: the reference's (plane - o) * (1/d) for every slot (A/B)
+#endif
+constexpr float kFmaE2 = 0x1.04p-23f;   // >= 2 x 1.0002 u (+ the rounding of this product)
+constexpr float kFmaSure = 1.0000019f;  // 1 + 2^-19 > 1 + 6.0002 u: relative error of both ends
+__device__ __forceinline__ f2 slab2f(float b0, float b1, float p, float inv) {
+  return (f2){__builtin_fmaf(b0, inv, -p), __builtin_fmaf(b1, inv, -p)};
+}
+__device__ __forceinline__ bool ray_degenerate(const RayT& r) {
+  if (!ZRT_FMA_SLABS) return false;
+  const float pm = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.ox * r.ix), __builtin_fabsf(r.oy * r.iy)),
+                                   __builtin_fabsf(r.oz * r.iz));
+  return !(ray_m(r) < 0x1p100f) || !(pm < 0x1p120f);
+}
+
 struct SlotT {
   float en, ex;
 };
@@ -1126,9 +1154,22 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   int r0 = as_int(w.ra.x), r1 = as_int(w.ra.y), r2 = as_int(w.ra.z), r3 = as_int(w.ra.w);
   const float tb = __builtin_fabsf(best_t) * kOpen;
   const float m = ray_m(r), rel = ray_rel(r, m), slk = ray_slack(r, a.scene_extent, m);
+#if ZRT_FMA_SLABS
+  // slab distances fma(plane, 1/d, -p), p = o / d (see slab2f): E2 covers their error
+  const float px = r.ox * r.ix, py = r.oy * r.iy, pz = r.oz * r.iz;
+  const float pm = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(px), __builtin_fabsf(py)), __builtin_fabsf(pz));
+  const bool deg = !(m < 0x1p100f) || !(pm < 0x1p120f);  // ray_degenerate: nothing opens, wide_finish replays
+  const float E2 = pm * kFmaE2;
+#define ZRT_SLAB_X(V, A, B) slab2f(V.A, V.B, px, r.ix)
+#define ZRT_SLAB_Y(V, A, B) slab2f(V.A, V.B, py, r.iy)
+#define ZRT_SLAB_Z(V, A, B) slab2f(V.A, V.B, pz, r.iz)
+#else
+  constexpr bool deg = false;
+  constexpr float E2 = 0.0f;
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
+#endif
   f2 nx01 = ZRT_SLAB_X(w.nx, x, y), nx23 = ZRT_SLAB_X(w.nx, z, w);
   f2 ny01 = ZRT_SLAB_Y(w.ny, x, y), ny23 = ZRT_SLAB_Y(w.ny, z, w);
   f2 nz01 = ZRT_SLAB_Z(w.nz, x, y), nz23 = ZRT_SLAB_Z(w.nz, z, w);
@@ -1160,19 +1201,21 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   // narrowed test: entry > exit * rel (+ slack for a leaf slot) culls (ray_slack:
   // inner slots' boxes are stored grown, leaf slots' are the reference leaves');
   // widened slabs carry their margins already (rounding: 2^-16)
-  const float rl = pw ? 1.0000153f : rel, sl = pw ? 0.0f : slk;
-  const bool h0 = !(s0.en > __builtin_fmaf(s0.ex, rl, r0 < 0 ? sl : 0.0f));
-  const bool h1 = !(s1.en > __builtin_fmaf(s1.ex, rl, r1 < 0 ? sl : 0.0f));
-  const bool h2 = !(s2.en > __builtin_fmaf(s2.ex, rl, r2 < 0 ? sl : 0.0f));
-  const bool h3 = !(s3.en > __builtin_fmaf(s3.ex, rl, r3 < 0 ? sl : 0.0f));
+  const float rl = pw ? 1.0000153f : rel, sl = (pw ? 0.0f : slk) + E2;
+  const bool h0 = !deg && !(s0.en > __builtin_fmaf(s0.ex, rl, r0 < 0 ? sl : E2));
+  const bool h1 = !deg && !(s1.en > __builtin_fmaf(s1.ex, rl, r1 < 0 ? sl : E2));
+  const bool h2 = !deg && !(s2.en > __builtin_fmaf(s2.ex, rl, r2 < 0 ? sl : E2));
+  const bool h3 = !deg && !(s3.en > __builtin_fmaf(s3.ex, rl, r3 < 0 ? sl : E2));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
   }
   // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
   bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
-  const bool w0 = o0 && (pw || !(s0.en < s0.ex)), w1 = o1 && (pw || !(s1.en < s1.ex));
-  const bool w2 = o2 && (pw || !(s2.en < s2.ex)), w3 = o3 && (pw || !(s3.en < s3.ex));
+  // (certain: en < ex by the FMA distances' error; ZRT_FMA_SLABS = 0: kFmaSure is exact enough)
+#define ZRT_SURE(S) (__builtin_fmaf(S.en, ZRT_FMA_SLABS ? kFmaSure : 1.0f, E2) < S.ex)
+  const bool w0 = o0 && (pw || !ZRT_SURE(s0)), w1 = o1 && (pw || !ZRT_SURE(s1));
+  const bool w2 = o2 && (pw || !ZRT_SURE(s2)), w3 = o3 && (pw || !ZRT_SURE(s3));
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
     if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en);
     if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en);
@@ -1196,11 +1239,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #else
   if (__builtin_expect(__ballot(min(min(r0, r1), min(r2, r3)) < -kSphereSlotBias) != 0ull, 0)) {
 #endif
-#define ZRT_SPHERE_SLOT(K)                                                                    \
-  if (r##K < -kSphereSlotBias) {                                                              \
-    o##K = !pw && s##K.en < s##K.ex;                                                          \
-    if (!o##K && s##K.ex > 0.001f) o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);       \
-    r##K += kSphereSlotBias;                                                                  \
+#define ZRT_SPHERE_SLOT(K)                                                                                   \
+  if (r##K < -kSphereSlotBias) {                                                                             \
+    o##K = !pw && !deg && ZRT_SURE(s##K);                                                                    \
+    if (!o##K && !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, E2) > 0.001f)          \
+      o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);                                                   \
+    r##K += kSphereSlotBias;                                                                                 \
   }
     ZRT_SPHERE_SLOT(0)
     ZRT_SPHERE_SLOT(1)
@@ -1209,6 +1253,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #undef ZRT_SPHERE_SLOT
   }
 #endif
+#undef ZRT_SURE
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
   const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
   int32_t next = -1;
@@ -1282,7 +1327,10 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         open &= open - 1u;
         const int L = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
         const int pb = as_int(k == 0 ? rb.x : k == 1 ? rb.y : k == 2 ? rb.z : rb.w);
-        const float lp = ZRT_HAZARD_ENTRY ? (k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en) : -1.0f;
+        // the leaf's loose entry, or (FMA distances) an upper bound of it: flags a superset
+        const float lp = ZRT_HAZARD_ENTRY ? (ZRT_FMA_SLABS ? __builtin_fmaf(k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en, kFmaSure, E2)
+                                                           : (k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en))
+                                        : -1.0f;
         if (STATS) {
           const int f = __builtin_amdgcn_readfirstlane(L);
           coh.ptests += 1u;
@@ -1303,7 +1351,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
   if (L != 0) {                                                                                     \
     const int pb = as_int(RB);                                                                      \
-    const float lp = ZRT_HAZARD_ENTRY ? s##K.en : -1.0f;                                              \
+    const float lp = ZRT_HAZARD_ENTRY ? (ZRT_FMA_SLABS ? __builtin_fmaf(s##K.en, kFmaSure, E2) : s##K.en) : -1.0f; \
     prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);              \
     if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp); \
   }
@@ -1362,7 +1410,7 @@ __device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, Stack
   // an origin farther out than the sphere growth was sized for: the reference's
   // way alone (narrow = false).  One call site for both cases: the replay is
   // inlined, and a second copy cost the lockstep loop 2.8 % on C4 (registers).
-  const bool far = __builtin_expect(!ray_origin_ok(a, r), 0);
+  const bool far = __builtin_expect(!ray_origin_ok(a, r) || ray_degenerate(r), 0);
   if (__builtin_expect((ZRT_ORDER_EXACT && order_hazard<false>(a, r, best_t, best)) || far, 0)) {
     if (STATS) ++c_replays;
 #if ZRT_REPLAY_OFF
@@ -1418,12 +1466,22 @@ __device__ __forceinline__ MatReg load_material(const DevMaterial* __restrict__ 
   return MatReg{q, q[1]};
 }
 
-// texture.zig:20-74
-__device__ __forceinline__ V3 albedo(const MatReg& mr, const KArgs& a, float u, float v) {
-  if (mr.tex_kind() == ZRT_TEX_COLOR) {
-    const float4 c = mr.q[0];
-    return mk(c.x, c.y, c.z);
-  }
+// Attenuation codes.  What Material.scatter returns as the attenuation
+// (material.zig:43-129) is one of: the (1,1,1) of a dielectric, a solid
+// texture's color (a material's), or one texel of an image texture
+// (texture.zig:20-74) - so a path stacks a 4-B code per scatter instead of
+// three floats, and an image texel is fetched only when the product is taken
+// (paths that end black never fetch theirs).  The values are the same f32s, so
+// the product (att_product) is bit for bit the recursion's.
+//   0xffffffff            dielectric (1, 1, 1)
+//   1 << 31 | material    the material's solid color
+//   1 << 30 | t           texel t of the f32 RGB store (a.texels)
+//   t                     texel t of the 8-bit store (a.texels8, values from a.lut255)
+// (t < 2^30: flatten_scene refuses larger stores)
+constexpr uint32_t kAttOne = 0xffffffffu;
+
+// texture.zig:20-74: the texel an image texture's albedo reads, as an att code
+__device__ __forceinline__ uint32_t image_texel_code(const MatReg& mr, float u, float v) {
   const float4 m2 = mr.q[2];
   struct { float u_off, v_off; uint32_t img_w, img_h, img_off, img_u8; } m = {
       mr.m1.x, mr.m1.y, __float_as_uint(m2.x), __float_as_uint(m2.y), __float_as_uint(m2.z), __float_as_uint(m2.w)};
@@ -1437,13 +1495,29 @@ __device__ __forceinline__ V3 albedo(const MatReg& mr, const KArgs& a, float u, 
   else if (uu_first < 0.0f) vv = vv_first + 1.0f;  // texture.zig:66 tests uu_first
   const uint32_t x = texel_index(uu * (float)m.img_w, m.img_w);
   const uint32_t y = texel_index(vv * (float)m.img_h, m.img_h);
-  const uint64_t t = (uint64_t)m.img_off + (uint64_t)y * m.img_w + x;
-  if (m.img_u8) {  // 4 B instead of 12 B per texel; the table holds the reference's f32 values
-    const uint32_t px = a.texels8[t];
-    return mk(a.lut255[px & 0xffu], a.lut255[(px >> 8) & 0xffu], a.lut255[(px >> 16) & 0xffu]);
+  const uint32_t t = m.img_off + y * m.img_w + x;  // < 2^30
+  return m.img_u8 ? t : (1u << 30) | t;
+}
+
+// The albedo of a lambertian / metal hit (texture.zig:20-74) as an att code
+__device__ __forceinline__ uint32_t albedo_code(const MatReg& mr, uint32_t mat, float u, float v) {
+  if (mr.tex_kind() == ZRT_TEX_COLOR) return (1u << 31) | mat;
+  return image_texel_code(mr, u, v);
+}
+
+// The attenuation an att code stands for
+__device__ __forceinline__ V3 att_value(const KArgs& a, const DevMaterial* __restrict__ mats, uint32_t code) {
+  if (code == kAttOne) return mk(1.0f, 1.0f, 1.0f);
+  if (code >> 31) {
+    const float4 c = reinterpret_cast<const float4*>(mats + (code & 0x7fffffffu))[0];
+    return mk(c.x, c.y, c.z);
   }
-  const float* p = a.texels + 3ull * t;
-  return mk(p[0], p[1], p[2]);
+  if (code >> 30) {
+    const float* p = a.texels + 3ull * (code & 0x3fffffffu);
+    return mk(p[0], p[1], p[2]);
+  }
+  const uint32_t px = a.texels8[code];  // 4 B instead of 12 B per texel; the table holds the reference's f32 values
+  return mk(a.lut255[px & 0xffu], a.lut255[(px >> 8) & 0xffu], a.lut255[(px >> 16) & 0xffu]);
 }
 
 // raytrace.zig:53-58
@@ -1514,8 +1588,10 @@ __device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ 
 // spilled to scratch)
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #else
 typedef float lds_float;
+typedef uint32_t lds_u32;
 #endif
 constexpr float kPi = 3.14159274101257324f;     // std.math.pi as f32
 constexpr float kTwoPi = 6.28318548202514648f;  // comptime 2*pi as f32
@@ -1537,12 +1613,12 @@ constexpr float kInvTwoPi = 1.0f / kTwoPi;
 // (hit_record.zig:28-41) + Material.scatter (material.zig:43-129): absorbed
 // ends the path black, a scatter pushes its attenuation (the product is taken
 // in the recursion's order when the path ends) and moves the ray on.
-// Where a path's attenuation rows live: rows 0 .. a.att_lds_rows-1 in LDS at
-// lds[(3 row + rgb) * lds_stride], the rest in global memory at
-// a.att[(row - a.att_lds_rows) * g_stride + g_index].  The lockstep and wavefront
-// loops index them by lane (stride kBlock / a.n_lanes), the path-pool loop by path.
+// Where a path's attenuation rows (att codes) live: rows 0 .. a.att_lds_rows-1
+// in LDS at lds[row * lds_stride], the rest in global memory at
+// a.att[(row - a.att_lds_rows) * g_stride + g_index].  The lockstep, wavefront and
+// list loops index them by lane (stride kBlock / a.n_lanes), the path-pool loop by path.
 struct AttRows {
-  lds_float* __restrict__ lds;
+  lds_u32* __restrict__ lds;
   uint32_t lds_stride;
   uint64_t g_index;
   uint32_t g_stride;
@@ -1551,16 +1627,17 @@ struct AttRows {
 // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
 // (raytrace.zig:99), over the n rows a path pushed, read back in reverse
 template <bool STATS>
-__device__ __forceinline__ V3 att_product(const KArgs& a, const AttRows& ar, uint32_t n, V3 col, Coh& coh) {
+__device__ __forceinline__ V3 att_product(const KArgs& a, const DevMaterial* __restrict__ mats, const AttRows& ar,
+                                          uint32_t n, V3 col, Coh& coh) {
   for (uint32_t i = n; i-- > 0;) {
-    V3 at;
+    uint32_t code;
     if (i < a.att_lds_rows) {
-      at = mk(ar.lds[(3 * i + 0) * ar.lds_stride], ar.lds[(3 * i + 1) * ar.lds_stride], ar.lds[(3 * i + 2) * ar.lds_stride]);
+      code = ar.lds[i * ar.lds_stride];
     } else {
-      const float4 g = a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
+      code = a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
       if (STATS) ++coh.attr;
-      at = mk(g.x, g.y, g.z);
     }
+    const V3 at = att_value(a, mats, code);
     col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
   }
   return col;
@@ -1636,7 +1713,8 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
     }
     // ---- Material.scatter (material.zig:43-129)
     bool absorbed = false;
-    V3 att = mk(1.0f, 1.0f, 1.0f), nd;
+    uint32_t att = kAttOne;  // the attenuation as an att code (dielectric: (1, 1, 1))
+    V3 nd;
     if (mkind == ZRT_MAT_LAMBERTIAN) {
       const float r1 = rand_float(rng);
       const float r2 = rand_float(rng);
@@ -1646,10 +1724,10 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
       V3 hv = mk(cs * rr, sn * rr, r1);
       if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
       nd = unit(add(normal, hv));
-      att = albedo(mat, a, tu, tv);
+      att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);
     } else if (mkind == ZRT_MAT_METAL) {
       nd = unit(reflect(unit(d), normal));
-      if (dot(nd, normal) > 0.0f) att = albedo(mat, a, tu, tv);
+      if (dot(nd, normal) > 0.0f) att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);
       else absorbed = true;
     } else {
       const float ratio = front ? dev::rcp_rn(mat.ior()) : mat.ior();
@@ -1673,11 +1751,9 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
         // the first rows live in LDS, deeper ones in global memory
         const uint32_t i = a.max_depth - depth_left;
         if (i < a.att_lds_rows) {
-          ar.lds[(3 * i + 0) * ar.lds_stride] = att.x;
-          ar.lds[(3 * i + 1) * ar.lds_stride] = att.y;
-          ar.lds[(3 * i + 2) * ar.lds_stride] = att.z;
+          ar.lds[i * ar.lds_stride] = att;
         } else {
-          a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = make_float4(att.x, att.y, att.z, 0.0f);
+          a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = att;
           if (STATS) ++coh.attw;
         }
       }
@@ -1695,7 +1771,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
-  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  lds_u32* att_l = (lds_u32*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][lane] att codes
   if (MODE == 3 && !layout_ok(a)) return;
   if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
@@ -1851,7 +1927,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     if (path_end) {
       // a path that reached the sky traced at depth_left >= 1: all of its
       // max_depth - depth_left scatters were pushed
-      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
+      const V3 col = sky ? att_product<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -1928,7 +2004,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
-  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  lds_u32* att_l = (lds_u32*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][lane] att codes
   if (!layout_ok(a)) return;
   if (ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
@@ -2034,7 +2110,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       }
     }
     if (path_end) {
-      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
+      const V3 col = sky ? att_product<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -2174,7 +2250,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
     pl.hit_p = (__attribute__((address_space(3))) int32_t*)(base + 7 * kBlockPaths);
     pl.queue = (__attribute__((address_space(3))) uint8_t*)(base + 8 * kBlockPaths) + wave_paths;
   }
-  lds_float* att_base = (lds_float*)(lds_raw + a.lds_att_off);  // [row][rgb][path of the block]
+  lds_u32* att_base = (lds_u32*)(lds_raw + a.lds_att_off);  // [row][path of the block] att codes
 
   // unit slots (wave-uniform): tile, chunk, the samples [.., unit_end) of the chunk
   bool slot_on[2] = {false, false};
@@ -2292,7 +2368,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
         }
         uint32_t smp = pA.sample();
         if (path_end) {
-          const V3 col = sky ? att_product<STATS>(a, ar, a.max_depth - dl, L, coh) : L;
+          const V3 col = sky ? att_product<STATS>(a, mats, ar, a.max_depth - dl, L, coh) : L;
           pA.acc_r += col.x;
           pA.acc_g += col.y;
           pA.acc_b += col.z;
@@ -2425,7 +2501,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
 template <int PRNG, bool STATS>
 __device__ __forceinline__ void render_loop_list(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  lds_float* att_l = (lds_float*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][rgb][lane]
+  lds_u32* att_l = (lds_u32*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][lane] att codes
   const DevMaterial* mats = a.mats;
   if (a.mats_in_lds) {  // block-uniform
     float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
@@ -2544,7 +2620,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
       scanline_add(a, py, 2, c_bg - bg0);
     }
     if (path_end) {
-      const V3 col = sky ? att_product<STATS>(a, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
+      const V3 col = sky ? att_product<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -2573,10 +2649,13 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 }
 
 #ifndef ZRT_ATT_ROWS_LIST
-#define ZRT_ATT_ROWS_LIST 8  // list loops (MODE 0 / 6): attenuation rows kept in LDS (as many as their 6-block share holds)
+#define ZRT_ATT_ROWS_LIST 24  // list loops (MODE 0 / 6): attenuation rows kept in LDS (as many as their 6-block share holds)
+#endif
+#ifndef ZRT_ATT_ROWS_LOCK
+#define ZRT_ATT_ROWS_LOCK 6  // lockstep FAST loop: attenuation rows kept in LDS (6 KiB per block, as 2 rows of 3 floats were)
 #endif
 #ifndef ZRT_ATT_ROWS_WF
-#define ZRT_ATT_ROWS_WF 4  // wavefront loop: attenuation rows kept in LDS (A/B: 2 = the lockstep kernel's)
+#define ZRT_ATT_ROWS_WF 12  // wavefront loop: attenuation rows kept in LDS (12 KiB per block, as 4 rows of 3 floats were)
 #endif
 #ifndef ZRT_WAVES_WF
 #define ZRT_WAVES_WF 4  // wavefront loop (MODE 4)
@@ -2586,7 +2665,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 #define ZRT_WAVES_POOL 4  // path-pool loop (MODE 5)
 #endif
 #ifndef ZRT_ATT_ROWS_POOL
-#define ZRT_ATT_ROWS_POOL 1  // path-pool loop: attenuation rows kept in LDS per path (6 KiB per row per block)
+#define ZRT_ATT_ROWS_POOL 3  // path-pool loop: attenuation rows kept in LDS per path (2 KiB per row per block)
 #endif
 
 template <int MODE, int PRNG, bool STATS, class StackT>
@@ -2976,7 +3055,7 @@ struct zrt_ctx {
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
   float tri_c[3] = {0.0f, 0.0f, 0.0f}, tri_h[3] = {0.0f, 0.0f, 0.0f};  // KArgs::tri_c / tri_h
-  zrt::DevBuf<float4> att;
+  zrt::DevBuf<uint32_t> att;  // attenuation rows past the LDS ones (att codes)
   zrt::DevBuf<uint8_t> stack_ovf;  // FAST stack rows beyond the LDS part (deep trees)
   zrt::DevBuf<unsigned long long> scratch;  // counters, work counter, error flag (kScratchSlots)
   zrt::DevBuf<float4> partial;
@@ -3286,8 +3365,8 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     img_off[i] = count;
     count += uint64_t(im.width) * im.height;
   }
-  if (texel_count >= (1ull << 32) || texel8_count >= (1ull << 32))
-    throw Error(ZRT_E_UNSUPPORTED, "more than 2^32 texels");
+  if (texel_count >= (1ull << 30) || texel8_count >= (1ull << 30))  // (att codes carry a 30-bit texel index)
+    throw Error(ZRT_E_UNSUPPORTED, "more than 2^30 texels in one store");
   for (uint32_t i = 0; i < s->n_materials; ++i) {
     const zrt_material& m = s->materials[i];
     DevMaterial dm{};
@@ -3469,17 +3548,18 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   // block of exactly 32 KiB ran 8 % slower at 5 blocks per CU)
   const size_t budget = (160u << 10) / waves - (1u << 10);
   const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-  const size_t row_att = 3 * sizeof(float) * (pool ? kBlockPaths : kBlock);
+  const size_t row_att = sizeof(uint32_t) * (pool ? kBlockPaths : kBlock);  // one att code per lane / path
   const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * kOctCopies : 0;
   const size_t pool_b = pool ? kPoolLdsBytes : 0;
-  // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1)
-  // A/B (C4, interleaved): none 50.35, 1 row 50.57, 2 rows 50.70 Gray/s; 4 rows
-  // (a 32 KiB block, the whole budget) 46.5
-  // The wavefront loop runs 4 blocks per CU: its larger share holds 4 rows (its
-  // scenes, the textured C5 mesh, scatter more often)
-  // The list loop (mode 0: no stack, no tree in LDS) keeps up to 8 rows: C2 (depth
-  // 30, glass) 32.7 -> 33.3 (4 rows) -> 34.0 Gray/s (8 rows), profiles/r03/ab12
-  const uint32_t att_cap = pool ? ZRT_ATT_ROWS_POOL : wf ? ZRT_ATT_ROWS_WF : mode == 0 ? ZRT_ATT_ROWS_LIST : 2u;
+  // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1).
+  // A row is one 4-B att code per lane (att_code; round 3: three floats, 12 B), so
+  // the same LDS holds three times the rows: the lockstep loop 6 (round 3, 2 rows
+  // of floats - C4 A/B: none 50.35, 1 row 50.57, 2 rows 50.70 Gray/s; a 32 KiB
+  // block 46.5), the wavefront loop 12 (its 4 blocks per CU have a larger share;
+  // the textured C5 mesh scatters often), the path pool 3 per path, the list loops
+  // 24 (no stack, no tree in LDS; C2 at depth 30 with glass: round 3 2 -> 4 -> 8
+  // rows of floats 32.7 -> 33.3 -> 34.0 Gray/s, profiles/r03/ab12)
+  const uint32_t att_cap = pool ? ZRT_ATT_ROWS_POOL : wf ? ZRT_ATT_ROWS_WF : mode == 0 ? ZRT_ATT_ROWS_LIST : ZRT_ATT_ROWS_LOCK;
   uint32_t want = att_cap;
   if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
@@ -3853,7 +3933,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint64_t n_paths = pool ? uint64_t(grid) * zrt::kBlockPaths : n_lanes;
     if (n_paths >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "too many paths");
     const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_paths;
-    if (att_need * sizeof(float4) > (16ull << 30))
+    if (att_need * sizeof(uint32_t) > (16ull << 30))
       return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
     if (c->att.n < att_need) c->att.alloc(att_need);
     HIPCHK(hipMemsetAsync(c->scratch.p, 0, zrt::kScratchSlots * sizeof(unsigned long long), st));
