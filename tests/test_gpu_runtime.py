@@ -325,3 +325,28 @@ def test_stats_report_the_sampling_loop(scenes, scene_index, env, loop, monkeypa
     s = scenes(scene_index)
     _, st = z.render(s, s.camera, z.RenderParams(16, 16, 1, 4))
     assert st["sampling_loop"] == loop
+
+
+def test_distant_camera_triangle_scene_does_not_replay(scenes):
+    """in a scene without spheres no ray needs the
+    sphere-slot origin bound, so a camera far outside the scene's box no longer
+    sends every ray to the reference replay.  The bunny's triangles alone (no
+    ground sphere) seen from 30x the model's size away: the frame equals the
+    oracle's bit for bit and order replays stay a tiny fraction of the rays."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import hazard_rays as H
+    from test_gpu_parity import prim_array
+    pr = prim_array(scenes(2).view.contents)
+    tri = pr[pr["kind"] == _ffi.ZRT_PRIM_TRIANGLE]
+    scene = H.scene_of([], [(t["a"], t["b"], t["c"]) for t in tri])
+    pts = np.concatenate([tri["a"], tri["b"], tri["c"]]).reshape(-1, 3)
+    ctr = (pts.min(0) + pts.max(0)) / 2
+    size = float(np.max(pts.max(0) - pts.min(0)))
+    cam = z.camera_init(ctr + np.array([0.3, 0.2, 30.0]) * size, ctr, (0, 1, 0), 2.5, 1.0)
+    p = z.RenderParams(48, 48, 4, 4, flags=z.ZRT_FLAG_STATS)
+    img, st = z.render(scene, cam, p)
+    ref, rs = O.render(scene, cam, p)
+    assert same_bits(img, ref)
+    assert st["rays_processed"] == rs["rays_processed"]
+    assert st["order_replays"] <= 0.01 * st["rays_processed"], st["order_replays"]
