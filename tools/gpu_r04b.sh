@@ -22,3 +22,7 @@ done
 bash tools/gpu_env_ab.sh r04b/c3 1 "ZRT_GRAZE_M=0" "ZRT_GRAZE_M=0.00006103515625" "ZRT_GRAZE_M=0.0009765625" "ZRT_GRAZE_M=0.015625" -- $C3 || exit 1
 bash tools/gpu_env_ab.sh r04b/c4 1 "ZRT_GRAZE_M=0" "ZRT_GRAZE_M=0.00006103515625" "ZRT_GRAZE_M=0.0009765625" "ZRT_GRAZE_M=0.015625" -- --no-reference-check || exit 1
 echo session-done
+# the full C3 frame with the REFERENCE traversal beside FAST (frame hashes)
+timeout -k 10 900 python bench.py --scene 3 --width 1024 --height 1024 --spp 256 --depth 20 --no-cpu-baseline > $O/c3_ref.json 2> $O/c3_ref.err || { tail -5 $O/c3_ref.err; exit 1; }
+python -c "import json; d=json.load(open('$O/c3_ref.json')); print('C3', d['value'], d['reference_traversal'])"
+echo session-done-2

@@ -123,6 +123,7 @@ struct KArgs {
                            // on the host, and scattered rays start at hits), so ray_origin_ok is skipped
   uint32_t layout;         // the wide tree's encoding (accel_build.hpp kLayout*): must equal kKernelLayout
   float graze_m;           // the grazing margins' coefficient (RayT::gm; DESIGN.md §3 "Grazing rays")
+  float graze_leaf;        // ... of leaf slots' relative margin (RayT::gl, >= graze_m)
 };
 
 // error_flag bits (zrt_ctx_sync / zrt_ctx_stats / zrt_render report them as ZRT_E_UNSUPPORTED)
@@ -345,9 +346,9 @@ struct RayT {
   // triangle.zig:61 that passes det >= 1e-6 lies in dev::rcp_core's range; a
   // wave-uniform value (from KArgs), so the choice below is a scalar branch
   uint32_t rcp_det;
-  // the scene's grazing-margin coefficient (KArgs::graze_m, 2^-18 by default):
-  // wave-uniform, so it stays in an SGPR
-  float gm;
+  // the scene's grazing-margin coefficients (KArgs::graze_m / graze_leaf, 2^-18 by
+  // default): inner slots / leaf slots; wave-uniform, so they stay in SGPRs
+  float gm, gl;
 };
 
 // A computed primitive hit lies outside its own box: a triangle's by a few ulps
@@ -406,6 +407,9 @@ __device__ __forceinline__ float ray_slack(const RayT& r, float extent, float m)
 // the triangles' largest |coordinate|, ray_slack's spatial term) - 6 more adds
 // per slot, for waves with such a lane only; the other waves keep ray_rel with
 // m <= kPaxisM.
+#ifndef ZRT_GRAZE_LEAF
+#define ZRT_GRAZE_LEAF 1  // leaf slots' relative margin from its own coefficient (KArgs::graze_leaf; A/B of a leaf-only guard)
+#endif
 #ifndef ZRT_PAXIS
 #define ZRT_PAXIS 1  // 0: A/B only (every wave on the t-space margins of ray_rel / ray_slack)
 #endif
@@ -996,7 +1000,7 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   // the narrowed test of the box grown by g (NaN bounds constrain nothing)
   const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
   const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
-  return loose && !(en > ex * ray_rel(r, ray_m(r)));
+  return loose && !(en > ex * (ZRT_GRAZE_LEAF ? 1.0000153f + r.gl * ray_m(r) : ray_rel(r, ray_m(r))));
 }
 
 // static_ok of leaf slot k, its slab distances recomputed from the node in memory
@@ -1202,10 +1206,15 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   // inner slots' boxes are stored grown, leaf slots' are the reference leaves');
   // widened slabs carry their margins already (rounding: 2^-16)
   const float rl = pw ? 1.0000153f : rel, sl = (pw ? 0.0f : slk) + E2;
-  const bool h0 = !deg && !(s0.en > __builtin_fmaf(s0.ex, rl, r0 < 0 ? sl : E2));
-  const bool h1 = !deg && !(s1.en > __builtin_fmaf(s1.ex, rl, r1 < 0 ? sl : E2));
-  const bool h2 = !deg && !(s2.en > __builtin_fmaf(s2.ex, rl, r2 < 0 ? sl : E2));
-  const bool h3 = !deg && !(s3.en > __builtin_fmaf(s3.ex, rl, r3 < 0 ? sl : E2));
+#if ZRT_GRAZE_LEAF
+  const float rll = pw ? 1.0000153f : 1.0000153f + r.gl * m;  // leaf slots (KArgs::graze_leaf)
+#else
+  const float rll = rl;
+#endif
+  const bool h0 = !deg && !(s0.en > __builtin_fmaf(s0.ex, r0 < 0 ? rll : rl, r0 < 0 ? sl : E2));
+  const bool h1 = !deg && !(s1.en > __builtin_fmaf(s1.ex, r1 < 0 ? rll : rl, r1 < 0 ? sl : E2));
+  const bool h2 = !deg && !(s2.en > __builtin_fmaf(s2.ex, r2 < 0 ? rll : rl, r2 < 0 ? sl : E2));
+  const bool h3 = !deg && !(s3.en > __builtin_fmaf(s3.ex, r3 < 0 ? rll : rl, r3 < 0 ? sl : E2));
   if (STATS) {
     ++c_nodes;
     c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
@@ -1890,6 +1899,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
       r.rcp_det = a.tri_rcp_fast;
       r.gm = a.graze_m;
+      r.gl = a.graze_leaf;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
             float best_t = __builtin_inff();
       int best = -1;
@@ -2030,6 +2040,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   RayT r{};
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
+  r.gl = a.graze_leaf;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2271,6 +2282,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   RayT r{};
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
+  r.gl = a.graze_leaf;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2493,10 +2505,11 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
 // (C2: 2.14 rays per sample, glass paths up to depth 30; VALU lane utilisation
 // 0.31).  Here a work item is one (pixel, chunk) - the 64 items of a unit are
 // the 64 pixels of its tile - and each lane runs its own item's samples in
-// order and takes the next item as soon as it is done: the lanes of a wave
-// needing one share one atomic (ballot + mbcnt rank).  The chunk's sum is the
-// same sequential sum in the same slot, so images are bit-identical to the
-// other loops'.
+// order and takes the next item as soon as it is done: the wave claims a unit
+// (one atomic) and hands its pixels to its lanes as they free up (ballot +
+// mbcnt rank), so no lane waits for another.  The chunk's sum is the same
+// sequential sum in the same slot, so images are bit-identical to the other
+// loops'.
 // ---------------------------------------------------------------------------
 template <int PRNG, bool STATS>
 __device__ __forceinline__ void render_loop_list(const KArgs& a) {
@@ -2518,10 +2531,11 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 #endif
   const int lane = (int)__lane_id();
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t total_items = a.total_work * 64u;  // < 2^32 (host check on tiles x 64 x chunks)
 
   bool has = false, in_sample = false;  // this lane holds an item / one of its samples is under way
-  bool exhausted = false;               // wave-uniform: every item has been handed out
+  bool exhausted = false;               // wave-uniform: the unit counter ran out
+  // the wave's current unit (wave-uniform): tile, chunk, corner, next pixel to hand out (64: none left)
+  uint32_t u_lt = 0, u_chunk = 0, u_x0 = 0, u_y0 = 0, u_next = 64;
   uint32_t sample = 0, s_end = 0, slot = 0, px = 0, py = 0;
   float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
   V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -2532,38 +2546,55 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
   uint32_t c_loops = 0, c_lsteps = 0;
   Coh coh;  // STATS
   for (;;) {
-    // ---- refill: the lanes without an item take the next ones, one atomic per wave
+    // ---- refill: the lanes without an item take the next pixels of the wave's
+    // current unit (ballot + mbcnt rank); a unit runs dry -> the next one, one
+    // atomic per 64 items (an atomic per refill step ran the C2 frame at a
+    // quarter of the rate: one global counter for every wave's every step)
     const uint64_t need = __ballot(!has);
-    if (need != 0ull && !exhausted) {
+    if (need != 0ull && !(exhausted && u_next >= 64u)) {
+      const uint32_t rank =
+          (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       const uint32_t cnt = (uint32_t)__builtin_popcountll(need);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(a.work_counter, cnt);
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (base >= total_items || total_items - base <= cnt) exhausted = true;
-      if (!has) {
-        const uint32_t rank =
-            (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-        const uint32_t item = base + rank;  // (base + rank wraps only past total_items: no item then)
-        if (base < total_items && item < total_items) {
-          const uint32_t u = item >> 6, p = item & 63u;
-          const uint32_t ord = u / a.n_chunks, g = u - ord * a.n_chunks;
-          const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;
-          const uint32_t t = lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
-          px = (t % a.tiles_x) * 8u + (p & 7u);
-          py = (t / a.tiles_x) * 8u + (p >> 3);
+      uint32_t taken = 0;  // lanes served so far (by rank)
+#pragma unroll 1
+      for (int pass = 0; pass < 2 && taken < cnt; ++pass) {
+        if (u_next >= 64u) {  // the wave's unit is handed out: claim the next one
+          if (exhausted) break;
+          uint32_t u = 0;
+          if (lane == 0) u = atomicAdd(a.work_counter, 1u);
+          u = __builtin_amdgcn_readfirstlane(u);
+          if (u >= a.total_work) {
+            exhausted = true;
+            break;
+          }
+          const uint32_t ord = u / a.n_chunks;
+          u_chunk = u - ord * a.n_chunks;
+          u_lt = a.tile_order ? a.tile_order[ord] : ord;
+          const uint32_t t = u_lt * a.world + a.rank;  // local tile lt = global tile lt*world + rank
+          u_x0 = (t % a.tiles_x) * 8u;
+          u_y0 = (t / a.tiles_x) * 8u;
+          u_next = 0;
+        }
+        const uint32_t take = min(cnt - taken, 64u - u_next);
+        if (!has && rank >= taken && rank < taken + take) {
+          const uint32_t p = u_next + (rank - taken);
+          px = u_x0 + (p & 7u);
+          py = u_y0 + (p >> 3);
           if (px < a.xbound && py < a.height) {  // off-frame pixels: nothing (finalize writes black)
             has = true;
             in_sample = false;
-            sample = g * a.chunk;
+            sample = u_chunk * a.chunk;
             s_end = min(sample + a.chunk, a.spp);
-            slot = g * a.n_slots + lt * 64u + p;
+            slot = u_chunk * a.n_slots + u_lt * 64u + p;
             acc_r = acc_g = acc_b = 0.0f;
           }
         }
+        taken += take;
+        u_next += take;
       }
     }
     if (__ballot(has) == 0ull) {
-      if (exhausted) break;
+      if (exhausted && u_next >= 64u) break;
       continue;  // (every lane drew an off-frame pixel)
     }
     if (STATS) {
@@ -2598,6 +2629,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
       r.dx = d.x; r.dy = d.y; r.dz = d.z;
       r.rcp_det = a.tri_rcp_fast;
       r.gm = a.graze_m;
+      r.gl = a.graze_leaf;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
       float best_t = __builtin_inff();
       int best = -1;
@@ -2710,6 +2742,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   r.dx = d.x; r.dy = d.y; r.dz = d.z;
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
+  r.gl = a.graze_leaf;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
     float best_t = __builtin_inff();
   int best = -1;
@@ -3050,7 +3083,7 @@ struct zrt_ctx {
   zrt::DevBuf<uint8_t> ref_sph;
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;
   uint32_t layout = 0;  // the wide tree's encoding (KArgs::layout)
-  float graze_m = 0x1p-18f;  // KArgs::graze_m
+  float graze_m = 0x1p-18f, graze_leaf = 0x1p-18f;  // KArgs::graze_m / graze_leaf
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
@@ -3109,6 +3142,7 @@ struct HostScene {
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;  // KArgs::root_c / origin_bound
   uint32_t layout = 0;           // KArgs::layout: the wide tree's encoding
   float graze_m = 0x1p-18f;      // KArgs::graze_m (the inner boxes are grown by half of it)
+  float graze_leaf = 0x1p-18f;   // KArgs::graze_leaf
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
@@ -3132,6 +3166,11 @@ bool device_bvh(uint32_t n) {
 // ZRT_GRAZE_M overrides it (A/B of larger margins)
 float graze_margin() {
   if (const char* e = std::getenv("ZRT_GRAZE_M")) return std::max(0x1p-18f, float(std::atof(e)));
+  return 0x1p-18f;
+}
+
+float graze_leaf_margin() {  // ZRT_GRAZE_LEAF: leaf slots' coefficient (A/B of a leaf-only guard)
+  if (const char* e = std::getenv("ZRT_GRAZE_LEAF")) return std::max(0x1p-18f, float(std::atof(e)));
   return 0x1p-18f;
 }
 
@@ -3253,6 +3292,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     const float sphere_grow = any_sphere ? float(std::ldexp(std::sqrt(2.0), -9) * (3.0 * std::sqrt(3.0) + 1.0) * double(H)) : 0.0f;
     const double tw = now_ms();
     c->graze_m = graze_margin();
+    c->graze_leaf = std::max(c->graze_m, graze_leaf_margin());
     const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0.5f * c->graze_m : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
                                           ZRT_SPHERE_SLOTS != 0);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
@@ -3439,6 +3479,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->origin_bound = h.origin_bound;
   c->layout = h.layout;
   c->graze_m = h.graze_m;
+  c->graze_leaf = h.graze_leaf;
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -3988,6 +4029,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.origin_bound = c->origin_bound;
     a.layout = c->layout;
     a.graze_m = c->graze_m;
+    a.graze_leaf = c->graze_leaf;
     {  // the camera inside the bound: so is every ray of the launch (scattered rays start at hits)
       const float m = std::max({std::fabs(a.org[0] - a.root_c[0]), std::fabs(a.org[1] - a.root_c[1]),
                                 std::fabs(a.org[2] - a.root_c[2])});
@@ -4567,6 +4609,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.check_origins = 1;  // arbitrary ray origins
     a.layout = c->layout;
     a.graze_m = c->graze_m;
+    a.graze_leaf = c->graze_leaf;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
