@@ -168,13 +168,21 @@ typedef struct zrt_params {
  * counts BVH node visits, primitive tests, shaded hits and texel fetches
  * (zrt_stats).  Images are identical; the default flavour counts only the
  * Progress counters (raytrace.zig:20-34). */
-enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u, ZRT_FLAG_SCANLINES = 4u };
+enum { ZRT_FLAG_STATS = 1u, ZRT_FLAG_NO_SCHEDULE = 2u, ZRT_FLAG_SCANLINES = 4u, ZRT_FLAG_GUARD = 8u };
 enum { ZRT_DEFAULT_SAMPLE_CHUNK = 32u };
 /* Scheduling (FAST traversal, spp >= 128, unless ZRT_FLAG_NO_SCHEDULE): a probe
  * launch renders 1 sample per pixel of every tile (results discarded) and
  * records each tile's cost; the tiles are radix-sorted by descending cost on
  * the device and the render launch hands out units costliest first, so no long
  * unit starts at the end of the launch.  Images do not depend on it. */
+
+/* ZRT_FLAG_GUARD (FAST traversal): the grazing-triangle guard (DESIGN.md
+ * section 3 "Triangles"): every box is widened by the reach of the rounded
+ * triangle test (triangle.zig:48-70) for rays nearly parallel to a triangle,
+ * whose accepted hits can lie outside their leaf's box.  zrt_trace always uses
+ * it; a render uses it (in the path-pool loop) when this flag is set - the
+ * reference's scenes render bit for bit the same frames without it, at a third
+ * more speed on the teapot.  zrt_stats.guard reports the coefficient used. */
 
 /* ZRT_FLAG_SCANLINES: the launch also counts the recursion-limit hits,
  * reflections and background hits of every frame row (the deltas that
@@ -224,6 +232,8 @@ typedef struct zrt_stats {
    * binary / 2 reference BVH traversal, FAST traversal: 3 lockstep, 4 wavefront,
    * 5 path pool; 6 surface list with per-lane work items */
   uint32_t sampling_loop;
+  /* the grazing-triangle guard's coefficient of the launch (0: off; ZRT_FLAG_GUARD) */
+  float guard;
 } zrt_stats;
 
 /* One frame row's share of the Progress counters (raytrace.zig:20-34): what

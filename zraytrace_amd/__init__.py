@@ -19,7 +19,7 @@ import numpy as np
 from . import _ffi
 from ._ffi import (ZRT_PRNG_XOROSHIRO128, ZRT_PRNG_XOSHIRO256, ZRT_RNG_COUNTER,  # noqa: F401
                    ZRT_RNG_REFERENCE_STREAM, ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE,
-                   ZRT_TRAVERSAL_BINARY, ZRT_FLAG_STATS, ZRT_FLAG_NO_SCHEDULE, ZRT_FLAG_SCANLINES,
+                   ZRT_TRAVERSAL_BINARY, ZRT_FLAG_STATS, ZRT_FLAG_NO_SCHEDULE, ZRT_FLAG_SCANLINES, ZRT_FLAG_GUARD,
                    ZrtError, check)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -33,6 +33,7 @@ ZRT_TRAVERSAL_FAST, ZRT_TRAVERSAL_REFERENCE, ZRT_TRAVERSAL_BINARY = 0, 1, 2
 ZRT_FLAG_STATS = 1
 ZRT_FLAG_NO_SCHEDULE = 2
 ZRT_FLAG_SCANLINES = 4
+ZRT_FLAG_GUARD = 8
 
 
 class Vec3(C.Structure):
@@ -96,7 +97,7 @@ class Stats(C.Structure):
                 ("texel_bytes", C.c_uint32), ("schedule_ms", C.c_float),
                 ("order_replays", C.c_uint64), ("box_excess_max_triangle", C.c_float),
                 ("box_excess_max_sphere", C.c_float), ("box_excess_hits", C.c_uint64),
-                ("sampling_loop", C.c_uint32)]
+                ("sampling_loop", C.c_uint32), ("guard", C.c_float)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

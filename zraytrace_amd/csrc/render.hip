@@ -124,6 +124,7 @@ struct KArgs {
   uint32_t layout;         // the wide tree's encoding (accel_build.hpp kLayout*): must equal kKernelLayout
   float graze_m;           // the grazing margins' coefficient (RayT::gm; DESIGN.md §3 "Grazing rays")
   float graze_leaf;        // ... of leaf slots' relative margin (RayT::gl, >= graze_m)
+  float guard;             // the grazing-triangle guard (RayT::gk, wide_iter; 0: off)
 };
 
 // error_flag bits (zrt_ctx_sync / zrt_ctx_stats / zrt_render report them as ZRT_E_UNSUPPORTED)
@@ -349,6 +350,7 @@ struct RayT {
   // the scene's grazing-margin coefficients (KArgs::graze_m / graze_leaf, 2^-18 by
   // default): inner slots / leaf slots; wave-uniform, so they stay in SGPRs
   float gm, gl;
+  float gk;  // the grazing-triangle guard's coefficient (KArgs::guard; 0: off), wave-uniform
 };
 
 // A computed primitive hit lies outside its own box: a triangle's by a few ulps
@@ -408,7 +410,8 @@ __device__ __forceinline__ float ray_slack(const RayT& r, float extent, float m)
 // per slot, for waves with such a lane only; the other waves keep ray_rel with
 // m <= kPaxisM.
 #ifndef ZRT_GRAZE_LEAF
-#define ZRT_GRAZE_LEAF 1  // leaf slots' relative margin from its own coefficient (KArgs::graze_leaf; A/B of a leaf-only guard)
+#define ZRT_GRAZE_LEAF 0  // leaf slots' relative margin from its own coefficient (KArgs::graze_leaf; A/B of a
+                          // leaf-only guard: fixed none of the grazing-triangle misses, C4 -4 %, profiles/r04/r04c)
 #endif
 #ifndef ZRT_PAXIS
 #define ZRT_PAXIS 1  // 0: A/B only (every wave on the t-space margins of ray_rel / ray_slack)
@@ -430,13 +433,26 @@ __device__ __forceinline__ float paxis_grow(const KArgs& a, const RayT& r) {
 __device__ __forceinline__ float paxis_t(float g, float inv) {
   return __builtin_fminf(g * __builtin_fabsf(inv), 0x1p126f);
 }
+// The grazing-triangle guard's spatial widening for this ray: gk (T + extent)
+// (T as in paxis_grow bounds |o - a| for every triangle vertex a): the reach of
+// an accepted hit beyond its triangle, k |ao| + k_c (DESIGN.md §3 "Triangles").
+#ifndef ZRT_GUARD
+#define ZRT_GUARD 1
+#endif
+__device__ __forceinline__ float guard_grow(const KArgs& a, const RayT& r) {
+  const float T = (__builtin_fabsf(r.ox - a.tri_c[0]) + a.tri_h[0]) + (__builtin_fabsf(r.oy - a.tri_c[1]) + a.tri_h[1]) +
+                  (__builtin_fabsf(r.oz - a.tri_c[2]) + a.tri_h[2]);
+  return (T + __builtin_fmaxf(a.scene_extent, 0x1p-100f)) * (r.gk * 1.0000153f);
+}
 
 // aabb.zig:109-127: each axis against [t_min, t_max] on its own.
 // FAST additionally narrows the interval across axes (with a 2^-16 relative
 // margin) and reports the entry distance for near-first ordering.
+// gw: the grazing-triangle guard's spatial widening of the narrowed test (per
+// axis gw |1/d_k|; 0: none) - the loose test stays the reference's own
 template <bool FAST>
 __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const RayT& r, float t_max,
-                                         float* entry, float slack = 0.0f, bool narrow = true) {
+                                         float* entry, float slack = 0.0f, bool narrow = true, float gw = 0.0f) {
   const float t_min = 0.001f;
   float a0 = (lo.x - r.ox) * r.ix, a1 = (hi.x - r.ox) * r.ix;
   float b0 = (lo.y - r.oy) * r.iy, b1 = (hi.y - r.oy) * r.iy;
@@ -455,7 +471,14 @@ __device__ __forceinline__ bool box_test(const float4 lo, const float4 hi, const
   if (FAST) {
     const float en = __builtin_fmaxf(__builtin_fmaxf(an, bn), cn);
     const float ex = __builtin_fminf(__builtin_fminf(ax, bx), cx);
-    ok = ok && (!narrow || !(en > __builtin_fmaf(ex, ray_rel(r, ray_m(r)), slack)));
+    if (__builtin_expect(gw > 0.0f, 0)) {  // (a scalar branch: gw is the scene's guard)
+      const float wa = paxis_t(gw, r.ix), wb = paxis_t(gw, r.iy), wc = paxis_t(gw, r.iz);
+      const float enw = __builtin_fmaxf(__builtin_fmaxf(a0 - wa, b0 - wb), __builtin_fmaxf(c0 - wc, t_min));
+      const float exw = __builtin_fminf(__builtin_fminf(a1 + wa, b1 + wb), __builtin_fminf(c1 + wc, t_max));
+      ok = ok && (!narrow || !(enw > __builtin_fmaf(exw, ray_rel(r, ray_m(r)), slack)));
+    } else {
+      ok = ok && (!narrow || !(en > __builtin_fmaf(ex, ray_rel(r, ray_m(r)), slack)));
+    }
     *entry = en;
   }
   return ok;
@@ -714,6 +737,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
   const uint32_t rows = a.lds_rows, cap = a.ref_stack;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float slack = ray_slack(r, a.scene_extent, ray_m(r));
+  const float gw = ZRT_GUARD && r.gk > 0.0f ? guard_grow(a, r) : 0.0f;  // the grazing-triangle guard
   best_t = __builtin_inff();
   best = -1;
   uint32_t c_tri = 0, c_sph = 0;
@@ -728,7 +752,7 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
     // emptiness test (a box the ray does not cross holds no hit):
     // left-first with the reference's t_max, so every leaf is accepted or
     // rejected exactly as the reference does it, in ~1 % of its node visits
-    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e, slack, narrow && a.ref_sph[idx] == 0)) continue;
+    if (!box_test<ZRT_REPLAY_NARROW>(lo, hi, r, best_t, &e, slack, narrow && a.ref_sph[idx] == 0, gw)) continue;
     const int left = as_int(lo.w), right = as_int(hi.w);
     if (left < 0) {
       prim_test<false, false>(a.prims, left, r, best_t, best, c_tri, c_sph);
@@ -753,9 +777,9 @@ __device__ ZRT_REPLAY_ATTR void reference_replay(const KArgs& a, const RayT& r, 
 // test against t_max = +inf: the rounded sphere test reaches beyond the sphere
 // and its box by ~sqrt(u) |oc| and errs by as much in t (DESIGN.md §3 "Spheres").
 __device__ __forceinline__ bool binary_test(const KArgs& a, int idx, const float4 lo, const float4 hi, const RayT& r,
-                                            float tb, float* e, float slack) {
+                                            float tb, float* e, float slack, float gw) {
   if (a.ref_sph[idx]) return box_test<true>(lo, hi, r, __builtin_inff(), e, 0.0f, false);
-  return box_test<true>(lo, hi, r, tb, e, slack);
+  return box_test<true>(lo, hi, r, tb, e, slack, true, gw);
 }
 
 // Closest hit over the BVH.  FAST: near-first order with the narrowed slab
@@ -769,10 +793,11 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
   const uint32_t cap = a.stack_depth;
   if (FAST) {
     const float slack = ray_slack(r, a.scene_extent, ray_m(r));
+    const float gw = ZRT_GUARD && r.gk > 0.0f ? guard_grow(a, r) : 0.0f;  // the grazing-triangle guard
     float e;
     float4 lo = a.nodes[0], hi = a.nodes[1];
     if (STATS) ++c_nodes;
-    if (!binary_test(a, 0, lo, hi, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
+    if (!binary_test(a, 0, lo, hi, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack, gw)) {
       if (!ray_origin_ok(a, r)) reference_replay<StackT>(a, r, stk, 0u, best_t, best, false);
       return;
     }
@@ -787,8 +812,8 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         if (STATS) c_nodes += 2;
         const float tb = __builtin_fabsf(best_t) * kOpen + slack;
         float el, er;
-        const bool hl = binary_test(a, left, l0, l1, r, tb, &el, slack);
-        const bool hr = binary_test(a, right, r0, r1, r, tb, &er, slack);
+        const bool hl = binary_test(a, left, l0, l1, r, tb, &el, slack, gw);
+        const bool hr = binary_test(a, right, r0, r1, r, tb, &er, slack, gw);
         if (hl && hr) {
           const bool rfirst = er < el;
           const int far_idx = rfirst ? left : right;
@@ -808,7 +833,7 @@ __device__ __forceinline__ void traverse_bvh(const KArgs& a, const RayT& r, Stac
         const int idx = stk[sp * stride];
         const float4 p0 = a.nodes[2 * idx], p1 = a.nodes[2 * idx + 1];
         if (STATS) ++c_nodes;
-        if (binary_test(a, idx, p0, p1, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack)) {
+        if (binary_test(a, idx, p0, p1, r, __builtin_fabsf(best_t) * kOpen + slack, &e, slack, gw)) {
           left = as_int(p0.w);
           right = as_int(p1.w);
           found = true;
@@ -965,8 +990,11 @@ __device__ __forceinline__ bool static_ok(float nx, float ny, float nz, float fx
 // an <= en < ex <= ax on every axis): each axis on its own, its distances
 // recomputed from the node in memory (the same two roundings as the packed
 // form) so that none of them stays live across the node.
+// gg: the grazing-triangle guard's spatial widening of this ray (0: off), added to
+// the leaf's own slack in both tests; the entry stays the exact loose entry, so a
+// best hit found below it (a leaf opened only by the widening) is replayed.
 __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, const RayT& r, float tb,
-                                           bool sx, bool sy, bool sz, float& entry) {
+                                           bool sx, bool sy, bool sz, float& entry, float gg = 0.0f) {
   const float t_min = 0.001f;
   const float* f = reinterpret_cast<const float*>(q) + k;
 #if ZRT_OCT_COPIES
@@ -991,8 +1019,8 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
       __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(f[px]), __builtin_fabsf(f[qx])),
                       __builtin_fmaxf(__builtin_fabsf(f[py]), __builtin_fabsf(f[qy]))),
       __builtin_fmaxf(__builtin_fabsf(f[pz]), __builtin_fabsf(f[qz])));
-  const float g = cl * r.gm;
-  const float gx = g * __builtin_fabsf(r.ix), gy = g * __builtin_fabsf(r.iy), gz = g * __builtin_fabsf(r.iz);
+  const float g = __builtin_fmaf(cl, r.gm, gg);
+  const float gx = paxis_t(g, r.ix), gy = paxis_t(g, r.iy), gz = paxis_t(g, r.iz);
   const float tl = tb + __builtin_fmaxf(__builtin_fmaxf(gx, gy), gz);
   const bool loose = (__builtin_fminf(fx, tl) > __builtin_fmaxf(nx, t_min)) &&
                      (__builtin_fminf(fy, tl) > __builtin_fmaxf(ny, t_min)) &&
@@ -1163,17 +1191,42 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const float px = r.ox * r.ix, py = r.oy * r.iy, pz = r.oz * r.iz;
   const float pm = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(px), __builtin_fabsf(py)), __builtin_fabsf(pz));
   const bool deg = !(m < 0x1p100f) || !(pm < 0x1p120f);  // ray_degenerate: nothing opens, wide_finish replays
-  const float E2 = pm * kFmaE2;
-#define ZRT_SLAB_X(V, A, B) slab2f(V.A, V.B, px, r.ix)
-#define ZRT_SLAB_Y(V, A, B) slab2f(V.A, V.B, py, r.iy)
-#define ZRT_SLAB_Z(V, A, B) slab2f(V.A, V.B, pz, r.iz)
+  float E2 = pm * kFmaE2;
+  // The grazing-triangle guard (DESIGN.md §3 "Triangles"): every box widened on
+  // every axis by the reach g of the rounded triangle test, as w_k = g |1/d_k| in
+  // t, through the offsets of the FMA form (near planes - (p + w), far planes
+  // - (p - w)): no instruction per plane.  The exact interval then lies within
+  // [en, en + wm] .. [ex - wm, ex], so certain decisions need 2 wm more (Eg).
+  // (Two copies of the 24 distances under a scene-uniform branch: the offsets
+  // held across one copy cost the lockstep kernel 11 more spilled VGPRs.)
+  float Eg = E2, gg = 0.0f;  // gg: the guard's spatial widening (loose_slot), 0 when off
+  f2 nx01, nx23, ny01, ny23, nz01, nz23, fx01, fx23, fy01, fy23, fz01, fz23;
+#define ZRT_SLABS(PNX, PNY, PNZ, PFX, PFY, PFZ)                                                         \
+  nx01 = slab2f(w.nx.x, w.nx.y, PNX, r.ix); nx23 = slab2f(w.nx.z, w.nx.w, PNX, r.ix);                   \
+  ny01 = slab2f(w.ny.x, w.ny.y, PNY, r.iy); ny23 = slab2f(w.ny.z, w.ny.w, PNY, r.iy);                   \
+  nz01 = slab2f(w.nz.x, w.nz.y, PNZ, r.iz); nz23 = slab2f(w.nz.z, w.nz.w, PNZ, r.iz);                   \
+  fx01 = slab2f(w.fx.x, w.fx.y, PFX, r.ix); fx23 = slab2f(w.fx.z, w.fx.w, PFX, r.ix);                   \
+  fy01 = slab2f(w.fy.x, w.fy.y, PFY, r.iy); fy23 = slab2f(w.fy.z, w.fy.w, PFY, r.iy);                   \
+  fz01 = slab2f(w.fz.x, w.fz.y, PFZ, r.iz); fz23 = slab2f(w.fz.z, w.fz.w, PFZ, r.iz);
+  // (the wavefront, path-pool and trace loops only: in the lockstep kernel the branch
+  // alone cost 4 more spilled VGPRs, C4 -4 %, profiles/r04/r04d)
+  if (ZRT_GUARD && PAXIS && __builtin_expect(r.gk > 0.0f, 0)) {  // scene-uniform: a scalar branch
+    const float g = guard_grow(a, r);
+    gg = g;
+    const float wx = paxis_t(g, r.ix), wy = paxis_t(g, r.iy), wz = paxis_t(g, r.iz);
+    const float wm = __builtin_fmaxf(__builtin_fmaxf(wx, wy), wz);
+    E2 = (pm + wm) * kFmaE2;  // (the offsets p -+ w are rounded too)
+    Eg = __builtin_fmaf(wm, 2.0f, E2);
+    ZRT_SLABS(px + wx, py + wy, pz + wz, px - wx, py - wy, pz - wz)
+  } else {
+    ZRT_SLABS(px, py, pz, px, py, pz)
+  }
+#undef ZRT_SLABS
 #else
-  constexpr bool deg = false;
-  constexpr float E2 = 0.0f;
+  constexpr float Eg = 0.0f;
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
-#endif
   f2 nx01 = ZRT_SLAB_X(w.nx, x, y), nx23 = ZRT_SLAB_X(w.nx, z, w);
   f2 ny01 = ZRT_SLAB_Y(w.ny, x, y), ny23 = ZRT_SLAB_Y(w.ny, z, w);
   f2 nz01 = ZRT_SLAB_Z(w.nz, x, y), nz23 = ZRT_SLAB_Z(w.nz, z, w);
@@ -1183,6 +1236,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #undef ZRT_SLAB_X
 #undef ZRT_SLAB_Y
 #undef ZRT_SLAB_Z
+#endif
   // a lane of the wave runs nearly parallel to an axis (paxis_grow): every slab
   // widened in place by its axis's own term; the leaf slots' exact intervals (the
   // reference's loose test, the hazard entry) are then recomputed by loose_slot
@@ -1222,14 +1276,17 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   // leaf slots that pass both tests: their primitive refs (a in r_k, b in the node's last float4)
   bool o0 = r0 < 0 && h0, o1 = r1 < 0 && h1, o2 = r2 < 0 && h2, o3 = r3 < 0 && h3;
   // (certain: en < ex by the FMA distances' error; ZRT_FMA_SLABS = 0: kFmaSure is exact enough)
-#define ZRT_SURE(S) (__builtin_fmaf(S.en, ZRT_FMA_SLABS ? kFmaSure : 1.0f, E2) < S.ex)
-  const bool w0 = o0 && (pw || !ZRT_SURE(s0)), w1 = o1 && (pw || !ZRT_SURE(s1));
-  const bool w2 = o2 && (pw || !ZRT_SURE(s2)), w3 = o3 && (pw || !ZRT_SURE(s3));
+#define ZRT_SURE(S) (__builtin_fmaf(S.en, ZRT_FMA_SLABS ? kFmaSure : 1.0f, Eg) < S.ex)
+  // (guarded: the slabs are widened, so every opened leaf takes its exact loose entry - the
+  // hazard test's E - and its widened per-axis tests from memory)
+  const bool pg = pw || gg > 0.0f;
+  const bool w0 = o0 && (pg || !ZRT_SURE(s0)), w1 = o1 && (pg || !ZRT_SURE(s1));
+  const bool w2 = o2 && (pg || !ZRT_SURE(s2)), w3 = o3 && (pg || !ZRT_SURE(s3));
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en);
-    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en);
-    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz, s2.en);
-    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz, s3.en);
+    if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en, gg);
+    if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en, gg);
+    if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz, s2.en, gg);
+    if (w3) o3 = loose_slot(q, 3, r, tb, sx, sy, sz, s3.en, gg);
   }
 #if ZRT_SPHERE_SLOTS
   // leaf slots holding a sphere (ref a - 2^30, accel_build.hpp): opened when the
@@ -1251,7 +1308,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #define ZRT_SPHERE_SLOT(K)                                                                                   \
   if (r##K < -kSphereSlotBias) {                                                                             \
     o##K = !pw && !deg && ZRT_SURE(s##K);                                                                    \
-    if (!o##K && !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, E2) > 0.001f)          \
+    if (!o##K && !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, Eg) > 0.001f)          \
       o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);                                                   \
     r##K += kSphereSlotBias;                                                                                 \
   }
@@ -1337,6 +1394,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         const int L = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
         const int pb = as_int(k == 0 ? rb.x : k == 1 ? rb.y : k == 2 ? rb.z : rb.w);
         // the leaf's loose entry, or (FMA distances) an upper bound of it: flags a superset
+        // (a guarded leaf's entry is exact: it went through loose_slot)
         const float lp = ZRT_HAZARD_ENTRY ? (ZRT_FMA_SLABS ? __builtin_fmaf(k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en, kFmaSure, E2)
                                                            : (k == 0 ? s0.en : k == 1 ? s1.en : k == 2 ? s2.en : s3.en))
                                         : -1.0f;
@@ -1900,6 +1958,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       r.rcp_det = a.tri_rcp_fast;
       r.gm = a.graze_m;
       r.gl = a.graze_leaf;
+      r.gk = a.guard;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
             float best_t = __builtin_inff();
       int best = -1;
@@ -2041,6 +2100,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
   r.gl = a.graze_leaf;
+  r.gk = a.guard;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2283,6 +2343,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
   r.gl = a.graze_leaf;
+  r.gk = a.guard;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2630,6 +2691,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
       r.rcp_det = a.tri_rcp_fast;
       r.gm = a.graze_m;
       r.gl = a.graze_leaf;
+      r.gk = a.guard;
       inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
       float best_t = __builtin_inff();
       int best = -1;
@@ -2743,6 +2805,7 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
   r.gl = a.graze_leaf;
+  r.gk = a.guard;
   inv_dir(d.x, d.y, d.z, r.ix, r.iy, r.iz);
     float best_t = __builtin_inff();
   int best = -1;
@@ -3084,6 +3147,7 @@ struct zrt_ctx {
   float root_c[3] = {0.0f, 0.0f, 0.0f}, origin_bound = 0.0f;
   uint32_t layout = 0;  // the wide tree's encoding (KArgs::layout)
   float graze_m = 0x1p-18f, graze_leaf = 0x1p-18f;  // KArgs::graze_m / graze_leaf
+  float guard = 0.0f;                                // KArgs::guard
   uint32_t texel_bytes = 0;
   uint32_t tri_rcp_fast = 1;
   float scene_extent = 1.0f;
@@ -3115,6 +3179,7 @@ struct zrt_ctx {
   bool last_stats = false;
   int last_mode = 0;
   int last_loop = 0;  // zrt_stats::sampling_loop
+  float last_guard = 0.0f;  // zrt_stats::guard
   int cu_count = 0;
   ~zrt_ctx() {
     if (ev_pre) (void)hipEventDestroy(ev_pre);
@@ -3143,6 +3208,7 @@ struct HostScene {
   uint32_t layout = 0;           // KArgs::layout: the wide tree's encoding
   float graze_m = 0x1p-18f;      // KArgs::graze_m (the inner boxes are grown by half of it)
   float graze_leaf = 0x1p-18f;   // KArgs::graze_leaf
+  float guard = 0.0f;            // KArgs::guard
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
@@ -3169,6 +3235,20 @@ float graze_margin() {
   return 0x1p-18f;
 }
 
+// The grazing-triangle guard's coefficient for a scene (DESIGN.md §3
+// "Triangles"): an accepted hit of the rounded test (triangle.zig:48-70) lies
+// outside its triangle by at most K u |ao| |e1||e2| / det, K = 2.6 the largest
+// measured (tools/tri_reach.py; 1.3 on the reference scenes' own triangles,
+// tools/tri_reach_bound.py gives the first-order worst case), and det >= 1e-6:
+// K u max |e1||e2| / 1e-6 per unit of |ao| <= T + extent (guard_grow).  Capped at
+// 2^-10 (above it the guard opens much of the tree; the teapot's model asks 0.024):
+// the grazing-triangle rays of every reference scene are exact from 2^-12
+// (profiles/r04/r04f).  ZRT_GUARD_K overrides it (A/B).
+float guard_model(double max_p12) {
+  if (const char* e = std::getenv("ZRT_GUARD_K")) return std::max(0.0f, float(std::atof(e)));
+  const double k = 2.6 * 0x1p-24 * max_p12 / 1e-6;
+  return float(std::min(k, double(0x1p-10)));
+}
 float graze_leaf_margin() {  // ZRT_GRAZE_LEAF: leaf slots' coefficient (A/B of a leaf-only guard)
   if (const char* e = std::getenv("ZRT_GRAZE_LEAF")) return std::max(0x1p-18f, float(std::atof(e)));
   return 0x1p-18f;
@@ -3293,6 +3373,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     const double tw = now_ms();
     c->graze_m = graze_margin();
     c->graze_leaf = std::max(c->graze_m, graze_leaf_margin());
+    c->guard = 0.0f;  // (set below, once the triangles are known)
     const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0.5f * c->graze_m : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
                                           ZRT_SPHERE_SLOTS != 0);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
@@ -3332,6 +3413,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   std::vector<float4> prims(3 * size_t(slot_to_prim.size()));
   std::vector<float4> shade(slot_to_prim.size());
   double tlo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, thi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  double tri_p12 = 0.0;  // the largest |e1| |e2| (guard_model)
   for (size_t sl = 0; sl < slot_to_prim.size(); ++sl) {
     const zrt_prim& p = s->prims[slot_to_prim[sl]];
     if (p.kind == ZRT_PRIM_TRIANGLE)  // ray_slack: the triangles' largest |coordinate|
@@ -3362,6 +3444,10 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
       // |det| = |d . n| <= |d| |n| < (1 + 2^-22) sqrt(3) 2^124 < 2^126 (NaN fails too)
       const float mn = std::max(std::fabs(nx), std::max(std::fabs(ny), std::fabs(nz)));
       if (!(mn < 0x1p124f)) c->tri_rcp_fast = 0;
+      // the grazing guard's model (guard_model): the largest |e1| |e2| of the scene
+      const double p12 = std::sqrt((double(e1x) * e1x + double(e1y) * e1y + double(e1z) * e1z) *
+                                   (double(e2x) * e2x + double(e2y) * e2y + double(e2z) * e2z));
+      if (p12 == p12) tri_p12 = std::max(tri_p12, p12);
     } else {
       q[0] = make_float4(p.center.x, p.center.y, p.center.z, p.radius * p.radius);  // sphere.zig:35 r*r, once
       q[1] = make_float4(0, 0, 0, 0);
@@ -3370,6 +3456,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     }
     std::memcpy(&sh.w, &tag, 4);
   }
+  if (use_bvh) c->guard = guard_model(tri_p12);
   // the triangles' bounding box as centre and half extents, rounded so that the
   // f32 box contains the exact one (paxis_grow); no triangle: an empty box at 0
   for (int k = 0; k < 3; ++k) {
@@ -3480,6 +3567,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->layout = h.layout;
   c->graze_m = h.graze_m;
   c->graze_leaf = h.graze_leaf;
+  c->guard = h.guard;
   c->upload_ms = now_ms() - t1;
   c->preprocess_ms = h.preprocess_ms;
   c->use_bvh = h.use_bvh;
@@ -3939,7 +4027,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // the path-pool loop (MODE 5) for the same cases, when asked for; a 16-bit stack
     // must fit beside its rays and queues in the block's LDS share, else the 32-bit
     // stack with overflow rows
-    const bool pool = mode == 3 && p->max_depth >= 1 && zrt::use_pool(c, stk16);
+    // the grazing-triangle guard (ZRT_FLAG_GUARD): carried by the path-pool loop's traversal
+    const bool guard_on = mode == 3 && (p->flags & ZRT_FLAG_GUARD) != 0 && c->guard > 0.0f;
+    const bool pool = mode == 3 && p->max_depth >= 1 && (zrt::use_pool(c, stk16) || guard_on);
     if (pool && stk16) {
       const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
       const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * zrt::kOctCopies : 0;
@@ -4030,6 +4120,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.layout = c->layout;
     a.graze_m = c->graze_m;
     a.graze_leaf = c->graze_leaf;
+    a.guard = guard_on ? c->guard : 0.0f;
     {  // the camera inside the bound: so is every ray of the launch (scattered rays start at hits)
       const float m = std::max({std::fabs(a.org[0] - a.root_c[0]), std::fabs(a.org[1] - a.root_c[1]),
                                 std::fabs(a.org[2] - a.root_c[2])});
@@ -4124,6 +4215,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_stats = diag;
     c->last_mode = mode;
     c->last_loop = kmode;
+    c->last_guard = a.guard;
     c->launched = 1;
     return ZRT_OK;
   }
@@ -4169,6 +4261,7 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
     out->wide_nodes = c->n_wide;
     out->sampling_loop = uint32_t(c->last_loop);
+    out->guard = c->last_guard;
     out->texel_bytes = c->texel_bytes;
     out->pixels_processed = c->last_pixels;
     out->samples_processed = uint64_t(c->last_pixels) * c->last_spp;
@@ -4610,6 +4703,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.layout = c->layout;
     a.graze_m = c->graze_m;
     a.graze_leaf = c->graze_leaf;
+    a.guard = c->guard;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
