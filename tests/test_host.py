@@ -291,3 +291,25 @@ def test_stats_struct_matches_header():
     names = re.findall(r"\b(?:u?int(?:32|64)_t|float|double)\s+(\w+)\s*;", body)
     assert names == [n for n, _ in _ffi.Stats._fields_]
 
+
+
+def test_u8_texel_values_by_short_division():
+    """render.hip att_value decodes an 8-bit texel k as dev::div_known(k, 255,
+    RN(1/255)) - q = RN(k y), r = fma(-q, 255, k), RN(r y + q) - instead of a table of
+    the reference's k / 255.0f (png_image.zig:88).  Checked here with exact rational
+    arithmetic for every k: the same f32 bits."""
+    from fractions import Fraction as F
+
+    def rn32(x):
+        f = np.float32(float(x))
+        cands = [np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))]
+        return min(cands, key=lambda c: (abs(F(float(c)) - x), int(np.float32(c).view(np.uint32)) & 1))
+
+    b = np.float32(255.0)
+    y = np.float32(1.0) / b
+    for k in range(256):
+        a = np.float32(k)
+        q = rn32(F(float(a)) * F(float(y)))
+        r = rn32(F(float(a)) - F(float(q)) * F(float(b)))
+        got = rn32(F(float(r)) * F(float(y)) + F(float(q)))
+        assert np.float32(got).view(np.uint32) == (np.float32(k) / b).view(np.uint32), k

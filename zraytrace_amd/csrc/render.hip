@@ -70,7 +70,6 @@ struct KArgs {
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;    // f32 RGB images
   const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
-  const float* __restrict__ lut255;      // k / 255.0f for k = 0..255 (png_image.zig:88)
   uint32_t* __restrict__ att;          // [row - att_lds_rows][lane or path]: attenuation codes (att_code)
   float4* __restrict__ partial;        // [chunk][tile slot] chunk sums
   uint32_t* __restrict__ work_counter;
@@ -1543,7 +1542,7 @@ __device__ __forceinline__ MatReg load_material(const DevMaterial* __restrict__ 
 //   0xffffffff            dielectric (1, 1, 1)
 //   1 << 31 | material    the material's solid color
 //   1 << 30 | t           texel t of the f32 RGB store (a.texels)
-//   t                     texel t of the 8-bit store (a.texels8, values from a.lut255)
+//   t                     texel t of the 8-bit store (a.texels8, values k / 255)
 // (t < 2^30: flatten_scene refuses larger stores)
 constexpr uint32_t kAttOne = 0xffffffffu;
 
@@ -1583,8 +1582,13 @@ __device__ __forceinline__ V3 att_value(const KArgs& a, const DevMaterial* __res
     const float* p = a.texels + 3ull * (code & 0x3fffffffu);
     return mk(p[0], p[1], p[2]);
   }
-  const uint32_t px = a.texels8[code];  // 4 B instead of 12 B per texel; the table holds the reference's f32 values
-  return mk(a.lut255[px & 0xffu], a.lut255[(px >> 8) & 0xffu], a.lut255[(px >> 16) & 0xffu]);
+  // 4 B instead of 12 B per texel.  Its values are k / 255 (png_image.zig:88): the
+  // correctly rounded quotient, which dev::div_known gives bit for bit for every
+  // k in 0..255 (checked exactly: tests/test_host.py) - no dependent table loads
+  const uint32_t px = a.texels8[code];
+  constexpr float kInv255 = 1.0f / 255.0f;  // RN(1/255)
+  return mk(dev::div_known(float(px & 0xffu), 255.0f, kInv255), dev::div_known(float((px >> 8) & 0xffu), 255.0f, kInv255),
+            dev::div_known(float((px >> 16) & 0xffu), 255.0f, kInv255));
 }
 
 // raytrace.zig:53-58
@@ -3140,7 +3144,7 @@ struct zrt_ctx {
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
-  zrt::DevBuf<float> texels, lut255;
+  zrt::DevBuf<float> texels;
   zrt::DevBuf<uint32_t> texels8;
   zrt::DevBuf<uint32_t> leaf_of_slot;
   zrt::DevBuf<uint8_t> ref_sph;
@@ -3212,7 +3216,7 @@ struct HostScene {
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
   std::vector<DevMaterial> mats;
-  std::vector<float> tex, lut;
+  std::vector<float> tex;
   std::vector<uint32_t> tex8;
   std::vector<uint32_t> slot_to_prim;  // device primitive slot -> reference list index
   std::vector<uint32_t> leaf_of_slot;  // device primitive slot -> its reference BVH leaf node
@@ -3540,7 +3544,6 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   c->mats = std::move(mats);
   c->tex = std::move(tex);
   c->tex8 = std::move(tex8);
-  c->lut.assign(lut, lut + 256);
   c->slot_to_prim = std::move(slot_to_prim);
   c->leaf_of_slot = std::move(leaf_of_slot);
   c->preprocess_ms = now_ms() - t0;
@@ -3559,7 +3562,6 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->mats.upload(h.mats);
   c->texels.upload(h.tex);
   c->texels8.upload(h.tex8);
-  c->lut255.upload(h.lut);
   c->leaf_of_slot.upload(h.leaf_of_slot);
   c->ref_sph.upload(h.ref_sph);
   for (int k = 0; k < 3; ++k) c->root_c[k] = h.root_c[k];
@@ -4076,7 +4078,6 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.mats = c->mats.p;
     a.texels = c->texels.p;
     a.texels8 = c->texels8.p;
-    a.lut255 = c->lut255.p;
     a.att = c->att.p;
     a.partial = c->partial.p;
     a.counters = c->scratch.p;
