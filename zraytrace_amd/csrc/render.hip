@@ -594,6 +594,9 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #ifndef ZRT_SCALAR_NODES
 #define ZRT_SCALAR_NODES 1  // FAST: a wide node every active lane reads next comes through the scalar cache
 #endif
+#ifndef ZRT_POOL_SCALAR
+#define ZRT_POOL_SCALAR 0  // path-pool loop: a node every traversing lane reads next comes through the scalar cache
+#endif
 #ifndef ZRT_SCALAR_PRIMS
 #define ZRT_SCALAR_PRIMS 1  // FAST: a primitive every active lane tests is read through the scalar cache
 #endif
@@ -1222,7 +1225,8 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   }
 #undef ZRT_SLABS
 #else
-  constexpr float Eg = 0.0f;
+  constexpr bool deg = false;
+  constexpr float E2 = 0.0f, Eg = 0.0f, gg = 0.0f;
 #define ZRT_SLAB_X(V, A, B) slab2(V.A, V.B, r.ox, r.ix)
 #define ZRT_SLAB_Y(V, A, B) slab2(V.A, V.B, r.oy, r.iy)
 #define ZRT_SLAB_Z(V, A, B) slab2(V.A, V.B, r.oz, r.iz)
@@ -2394,7 +2398,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, false, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
