@@ -1702,17 +1702,31 @@ struct AttRows {
 // attenuation_1 * (attenuation_2 * (... * L)): the recursion's association
 // (raytrace.zig:99), over the n rows a path pushed, read back in reverse
 template <bool STATS>
+__device__ __forceinline__ uint32_t att_row(const KArgs& a, const AttRows& ar, uint32_t i, Coh& coh) {
+  if (i < a.att_lds_rows) return ar.lds[i * ar.lds_stride];
+  if (STATS) ++coh.attr;
+  return a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
+}
+#ifndef ZRT_ATT_PAIRS
+#define ZRT_ATT_PAIRS 1  // att_product decodes two rows at a time (their texel loads in flight together)
+#endif
+template <bool STATS>
 __device__ __forceinline__ V3 att_product(const KArgs& a, const DevMaterial* __restrict__ mats, const AttRows& ar,
                                           uint32_t n, V3 col, Coh& coh) {
-  for (uint32_t i = n; i-- > 0;) {
-    uint32_t code;
-    if (i < a.att_lds_rows) {
-      code = ar.lds[i * ar.lds_stride];
-    } else {
-      code = a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
-      if (STATS) ++coh.attr;
+  uint32_t i = n;
+  // two rows per trip: both texel loads are issued before either product, so a
+  // textured path's chain of dependent fetches is half as long (the values and
+  // the order of the multiplications are the recursion's, as below)
+  if (ZRT_ATT_PAIRS) {
+    for (; i >= 2; i -= 2) {
+      const V3 hi = att_value(a, mats, att_row<STATS>(a, ar, i - 1, coh));
+      const V3 lo = att_value(a, mats, att_row<STATS>(a, ar, i - 2, coh));
+      col = mk(hi.x * col.x, hi.y * col.y, hi.z * col.z);
+      col = mk(lo.x * col.x, lo.y * col.y, lo.z * col.z);
     }
-    const V3 at = att_value(a, mats, code);
+  }
+  for (; i-- > 0;) {
+    const V3 at = att_value(a, mats, att_row<STATS>(a, ar, i, coh));
     col = mk(at.x * col.x, at.y * col.y, at.z * col.z);
   }
   return col;
