@@ -1680,7 +1680,8 @@ constexpr float kInvTwoPi = 1.0f / kTwoPi;
 #define ZRT_WAVES_LIST 6      // list mode (C2); A/B: w5 27.8, w6 30.3, w8 28.7 Gray/s
 #endif
 #ifndef ZRT_WAVES_WIDE
-#define ZRT_WAVES_WIDE 5      // FAST (wide tree) kernel; A/B (octant traversal, 96 VGPRs): w4 46.0, w5 50.6, w6 48.2 (spills) Gray/s
+#define ZRT_WAVES_WIDE 6      // FAST (wide tree) kernel, 80 VGPRs.  A/B, round 2 (96 VGPRs at w5): w4 46.0, w5 50.6,
+                              // w6 48.2 (spills); round 4 (4-B att codes): C4 w5 52.5, w6 55.1, w7 44.8; C3 15.1 / 15.1 / 13.4
 #endif
 
 // The rest of one rayColor step after its closest-hit query (raytrace.zig:
