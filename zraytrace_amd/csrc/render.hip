@@ -1170,7 +1170,7 @@ __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const Wid
 // the order-hazard test of wide_finish follows).  Its state between calls is
 // (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
-template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK>
+template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK, bool GUARD = true>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
                                           const float4*& q, uint32_t& sp, float& best_t, int& best,
@@ -1212,7 +1212,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   fz01 = slab2f(w.fz.x, w.fz.y, PFZ, r.iz); fz23 = slab2f(w.fz.z, w.fz.w, PFZ, r.iz);
   // (the wavefront, path-pool and trace loops only: in the lockstep kernel the branch
   // alone cost 4 more spilled VGPRs, C4 -4 %, profiles/r04/r04d)
-  if (ZRT_GUARD && PAXIS && __builtin_expect(r.gk > 0.0f, 0)) {  // scene-uniform: a scalar branch
+  if (ZRT_GUARD && GUARD && PAXIS && __builtin_expect(r.gk > 0.0f, 0)) {  // scene-uniform: a scalar branch
     const float g = guard_grow(a, r);
     gg = g;
     const float wx = paxis_t(g, r.ix), wy = paxis_t(g, r.iy), wz = paxis_t(g, r.iz);
@@ -2147,7 +2147,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       for (;;) {
         if (trav) {
           // (its lanes' nodes are rarely one: no scalar-load test, C5 -1.4 % with it)
-          if (!wide_iter<STATS, StackT, false, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, false, true, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             trav = false;
@@ -2319,7 +2319,14 @@ struct PoolLds {
   __attribute__((address_space(3))) uint8_t* queue;  // this wave's
 };
 
-template <int PRNG, bool STATS, class StackT>
+// Where a path's attenuation rows past LDS go: [path][row] keeps one path's rows in
+// one or two 32-B sectors, so its pushes of one sample (and the next samples') merge
+// in L2 before they are written back; [row][path] (0) spreads them, every 4-B code a
+// sector of its own (the pool's lanes shade paths at unrelated depths).
+#ifndef ZRT_POOL_ATT_PATH
+#define ZRT_POOL_ATT_PATH 1
+#endif
+template <int PRNG, bool STATS, class StackT, bool GUARD>
 __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the lane's traversal stack column
@@ -2345,6 +2352,8 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
     pl.queue = (__attribute__((address_space(3))) uint8_t*)(base + 8 * kBlockPaths) + wave_paths;
   }
   lds_u32* att_base = (lds_u32*)(lds_raw + a.lds_att_off);  // [row][path of the block] att codes
+  // global rows past the LDS ones: [path][row] (ZRT_POOL_ATT_PATH), g_rows per path
+  const uint32_t g_rows = a.max_depth > a.att_lds_rows ? a.max_depth - a.att_lds_rows : 1u;
 
   // unit slots (wave-uniform): tile, chunk, the samples [.., unit_end) of the chunk
   bool slot_on[2] = {false, false};
@@ -2366,7 +2375,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   r.rcp_det = a.tri_rcp_fast;
   r.gm = a.graze_m;
   r.gl = a.graze_leaf;
-  r.gk = a.guard;
+  r.gk = GUARD ? a.guard : 0.0f;
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
@@ -2413,7 +2422,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
@@ -2433,7 +2442,8 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
 #pragma unroll 1
     for (uint32_t s = 0; s < 2; ++s) {
       const uint32_t p = s * 64u + (uint32_t)lane, P = wave_paths + p;
-      const AttRows ar{att_base + P, kBlockPaths, g_paths + P, a.n_paths};
+      const AttRows ar = ZRT_POOL_ATT_PATH ? AttRows{att_base + P, kBlockPaths, (g_paths + P) * g_rows, 1u}
+                                           : AttRows{att_base + P, kBlockPaths, g_paths + P, a.n_paths};
       const uint32_t unit_end = s ? s_end[1] : s_end[0];
       const uint32_t x0 = s ? s_x0[1] : s_x0[0], y0 = s ? s_y0[1] : s_y0[0];
       bool push = false;
@@ -2786,14 +2796,15 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 #endif
 
 template <int MODE, int PRNG, bool STATS, class StackT>
-__global__ void __launch_bounds__(kBlock, MODE == 5   ? ZRT_WAVES_POOL
+__global__ void __launch_bounds__(kBlock, MODE == 5 || MODE == 7 ? ZRT_WAVES_POOL
                                           : MODE == 4 ? ZRT_WAVES_WF
                                           : MODE == 3 ? ZRT_WAVES_WIDE
                                           : MODE == 0 || MODE == 6 ? ZRT_WAVES_LIST
                                                       : ZRT_WAVES_PER_SIMD)
     render_kernel(const KArgs a) {
   if constexpr (MODE == 6) render_loop_list<PRNG, STATS>(a);
-  else if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT>(a);
+  else if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT, false>(a);
+  else if constexpr (MODE == 7) render_loop_pool<PRNG, STATS, StackT, true>(a);  // with the grazing-triangle guard
   else if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
   else render_loop<MODE, PRNG, STATS, StackT>(a);
 }
@@ -3664,6 +3675,7 @@ void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 3) return stk16 ? kernel_ptr<3, PRNG, STATS, uint16_t>() : kernel_ptr<3, PRNG, STATS, uint32_t>();
   if (mode == 4) return stk16 ? kernel_ptr<4, PRNG, STATS, uint16_t>() : kernel_ptr<4, PRNG, STATS, uint32_t>();
   if (mode == 5) return stk16 ? kernel_ptr<5, PRNG, STATS, uint16_t>() : kernel_ptr<5, PRNG, STATS, uint32_t>();
+  if (mode == 7) return stk16 ? kernel_ptr<7, PRNG, STATS, uint16_t>() : kernel_ptr<7, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
 void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
@@ -4057,7 +4069,9 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       if (size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) + top + zrt::kPoolLdsBytes > budget) stk16 = false;
     }
     const bool list_lanes = mode == 0 && zrt::use_list_lanes();
-    const int kmode = pool ? 5 : wf ? 4 : list_lanes ? 6 : mode;
+    // (the guard's branch costs the path pool 0.7 % on C5, so a guarded render has a
+    // kernel of its own, MODE 7; profiles/r04/r04n)
+    const int kmode = pool ? (guard_on ? 7 : 5) : wf ? 4 : list_lanes ? 6 : mode;
     void* kfn = zrt::select_kernel(kmode, p->prng, diag, stk16);
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
@@ -4081,7 +4095,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint64_t n_partial = uint64_t(my_tiles) * 64u * n_chunks;
     if (c->partial.n < n_partial) c->partial.alloc(n_partial);
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
-    // global attenuation rows: [row][lane], or [row][path] for the path-pool loop
+    // global attenuation rows: [row][lane], or [path][row] for the path-pool loop
     const uint64_t n_paths = pool ? uint64_t(grid) * zrt::kBlockPaths : n_lanes;
     if (n_paths >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "too many paths");
     const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_paths;
@@ -4234,7 +4248,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_xbound = g.xbound;
     c->last_stats = diag;
     c->last_mode = mode;
-    c->last_loop = kmode;
+    c->last_loop = kmode == 7 ? 5 : kmode;
     c->last_guard = a.guard;
     c->launched = 1;
     return ZRT_OK;
