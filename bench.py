@@ -373,7 +373,16 @@ def main():
         dc = fr.ctx.debug_counters(32)
         wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 4 * int(dc[28]),  # 4-B att codes
               "stack_rows_B": 4 * int(dc[30])}  # FAST stack entries past the LDS rows (kStackOvfWrites)
-        wb["predicted_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
+        wb["payload_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
+        # what memory sees: a chunk-sum store is 1 KiB of whole lines; a row or stack
+        # store is 4 B, and where the wave's lanes store to unrelated paths (every loop
+        # but lockstep, whose lanes push the same row together) each is written back as
+        # a 32-B sector of its own (L2 keeps no line long enough to merge a path's pushes
+        # under the C5 fetch stream: profiles/r04/r04o, path-major rows)
+        loop_id = int(st.get("sampling_loop", -1))
+        granule = 4 if loop_id == 3 else 32
+        wb["row_store_granule_B"] = granule
+        wb["predicted_B"] = wb["chunk_sums_B"] + (granule // 4) * (wb["att_rows_B"] + wb["stack_rows_B"])
         if pe and pe.get("write_size_kb"):
             wb["pmc_write_B"] = int(pe["write_size_kb"] * 1024)
             wb["predicted_over_pmc"] = round(wb["predicted_B"] / wb["pmc_write_B"], 3)
