@@ -22,7 +22,12 @@ by tools/ubench.hip (profiles/ubench.json); "bound" is the ceiling with the
 largest fraction.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
-     N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+     N > 1, one process per GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+     N > 1, one process for all GPUs (no launcher, WORLD_SIZE unset): python bench.py --gpus N
+       - zrt_multi_* over devices 0..N-1: one context per GPU, ncclCommInitAll
+       communicators and one ncclGather per frame inside libzrt (SURVEY §5);
+       --devices 0,0 rehearses it with two ranks on one GPU (device copies).
+       Fewer than N visible GPUs is an error (exit 2), never a silent N=1 line.
 """
 import argparse
 import hashlib
@@ -258,6 +263,112 @@ def reference_check(frame_obj, params, fast_sha1, z):
             "rays": st["rays_processed"], "frame_sha1": sha, "frame_equal_to_fast": sha == fast_sha1}
 
 
+def fail(msg, code=2):
+    log(f"bench.py: error: {msg}")
+    sys.exit(code)
+
+
+def main_multi(args, devices):
+    """--gpus N without a launcher: every GPU driven from this one process through
+    zrt_multi_* (per-device contexts, ncclCommInitAll, one ncclGather to
+    devices[0] and the assemble there).  A step = one zrt_multi_render: every
+    rank's launch enqueued, then the gather and assemble, synchronous; the frame
+    stays in devices[0]'s HBM (no PCIe copy in the timed region)."""
+    import torch
+    n_vis = torch.cuda.device_count()  # (counts without initialising a device)
+    if n_vis == 0 or max(devices) >= n_vis:
+        fail(f"--gpus {args.gpus} needs devices {sorted(set(devices))}, {n_vis} visible")
+    import zraytrace_amd as z
+    from zraytrace_amd.dist import tile_counts
+    scene = z.load_scene(args.scene)
+    trav = {"fast": z.ZRT_TRAVERSAL_FAST, "reference": z.ZRT_TRAVERSAL_REFERENCE,
+            "binary": z.ZRT_TRAVERSAL_BINARY}[args.traversal]
+    params = z.RenderParams(args.width, args.height, args.spp, args.depth, traversal=trav,
+                            sample_chunk=args.chunk)
+    m = z.MultiContext(scene, params, devices)
+    distinct = sorted(set(devices))
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        m.render(scene.camera, params, copy_out=False)
+        log(f"[multi] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f} s")
+    for d in distinct:
+        torch.cuda.synchronize(d)
+    rank_ms, gather_ms = [], []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        _, st = m.render(scene.camera, params, copy_out=False)
+        rank_ms.append(m.rank_ms())
+        gather_ms.append(st["gather_ms"])
+        log(f"[multi] step {i + 1}/{args.steps}: slowest rank kernel {max(rank_ms[-1]):.1f} ms, "
+            f"gather+assemble {gather_ms[-1]:.2f} ms")
+    for d in distinct:
+        torch.cuda.synchronize(d)
+    elapsed = time.perf_counter() - t0
+    frame_sha1 = hashlib.sha1(m.frame().tobytes()).hexdigest()
+    _, diag = m.render(scene.camera, z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS}),
+                       copy_out=False)
+    assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
+    m.close()
+
+    n = len(devices)
+    chunk = args.chunk or 32  # ZRT_DEFAULT_SAMPLE_CHUNK
+    counts = tile_counts(z.RenderParams(**{**params.__dict__, "world_size": n}))
+    n_units = sum(counts) * ((args.spp + chunk - 1) // chunk)
+    per_rank = [sum(r[k] for r in rank_ms) / len(rank_ms) for k in range(n)]
+    slowest_s = max(per_rank) / 1e3
+    algo = algorithmic_bytes(diag, n_units, diag["pixels_processed"])
+    # the ceilings are priced from PMC passes at N=1 only; here the frame's
+    # algorithmic bytes spread over the ranks against the slowest rank's kernel
+    roof = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+            "reason": "PMC passes are taken at N=1 only", "kernel_s": round(slowest_s, 6),
+            "algorithmic": {"bytes_per_launch": int(algo), "gbs_per_gpu": round(algo / n / slowest_s / 1e9, 1),
+                            "per_ray": {"node_visits": round(diag["node_visits"] / max(1, diag["rays_processed"]), 2),
+                                        "bytes": round(algo / max(1, diag["rays_processed"]), 1)}}}
+    key = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+           "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk}
+    ref_hash = n1_frame_hash(key)
+    out = {
+        "metric": METRIC,
+        "value": round(st["rays_processed"] * args.steps / elapsed / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": len(distinct),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: the reference's own scene {args.scene} ({SCENES[args.scene]}), no dataset",
+        "config": {"workload": f"scene {args.scene} ({SCENES[args.scene].split(':')[0]}) "
+                               f"{'BVH' if st['used_bvh'] else 'list'}, {args.width}x{args.height} @ "
+                               f"{args.spp} spp, max depth {args.depth}",
+                   "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+                   "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk,
+                   "rng": "counter (Xoroshiro128+ per pixel-sample, seed 42)",
+                   "parallelism": f"image tiles 8x8 round-robin over {n} rank(s) on devices {devices}, "
+                                  f"one process (zrt_multi_*), "
+                                  + ("ncclGather over xGMI" if len(distinct) == n and n > 1
+                                     else "device-to-device copies (ranks share a GPU)")},
+        "launcher": "none (one process, zrt_multi_*)",
+        "ranks": n,
+        "devices": devices,
+        "rays_per_step": int(st["rays_processed"]),
+        "samples_per_step": int(st["samples_processed"]),
+        "rays_per_sample": round(st["rays_processed"] / max(1, st["samples_processed"]), 4),
+        "kernel_ms_slowest_rank": round(max(per_rank), 2),
+        "roofline": roof,
+        "parity": "bit-exact vs oracle (tests/test_gpu_parity.py); frame vs the committed N=1 frame below",
+        "frame_sha1": frame_sha1,
+        "frame_sha1_n1": ref_hash,
+        "frame_equal_to_n1": (frame_sha1 == ref_hash) if ref_hash else None,
+        "build_id": z.build_id(),
+        "per_rank_ms": {"kernel": [round(x, 3) for x in per_rank],
+                        "gather_assemble": round(sum(gather_ms) / len(gather_ms), 3)},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,7 +387,18 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK)")
+    ap.add_argument("--devices", default=None,
+                    help="one-process path: comma-separated device per rank (e.g. 0,0 rehearses 2 ranks on GPU 0)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.devices):
+        devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+        if len(devices) < 1 or min(devices) < 0:
+            fail(f"--devices {args.devices}: need one non-negative device index per rank")
+        if not args.devices and len(devices) != args.gpus:
+            fail(f"--gpus {args.gpus} does not match {len(devices)} devices")
+        return main_multi(args, devices)
 
     import torch
     import torch.distributed as dist
@@ -285,7 +407,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        fail(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dist_backend == "nccl" and args.device is None:
+        n_vis = torch.cuda.device_count()
+        if local >= n_vis:
+            fail(f"rank {rank} needs GPU {local}, {n_vis} visible")
     if args.device is not None:
         local = args.device
     torch.cuda.set_device(local)
@@ -396,6 +522,17 @@ def main():
                 wb["pmc_wrreq_32B"] = int(n32)
                 wb["pmc_wrreq_bytes"] = int(64 * n64 + 32 * n32)
         roof["write_budget"] = wb
+        if pe and pe.get("fetch_size_kb") is not None:
+            # HBM bytes the sampling loop needs, apart from what spilled registers cost:
+            # the measured reads (2 x FETCH_SIZE KiB, MI355X_MICROARCH.md's gfx950
+            # correction) plus the predicted payload writes (chunk sums, global att and
+            # stack rows at the store granule), never the scratch lines of spills
+            useful = 2 * pe["fetch_size_kb"] * 1024 + wb["predicted_B"]
+            roof["useful_hbm"] = {"bytes_per_launch": int(useful),
+                                  "gbs": round(useful / avg_kernel_s / 1e9, 1),
+                                  "frac": round(useful / avg_kernel_s / (HBM_PEAK_GBS * 1e9), 4),
+                                  "note": "2 FETCH_SIZE (PMC) + predicted payload writes; hbm_frac also counts "
+                                          "spill scratch lines written back (WRITE_SIZE)"}
         # SIMD efficiency of the loop (STATS launch, zrt_ctx_debug_counters slots 4 / 21-23):
         # lane node visits / (64 x the wave's traversal trips), and the lanes that ran a
         # rayColor step / (64 x loop iterations that ran one)

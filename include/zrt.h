@@ -287,13 +287,22 @@ int zrt_render_multi(const zrt_scene* scene, const zrt_camera* camera,
  * the tiles move by device copies and RCCL is not loaded).
  * zrt_multi_render renders one frame as zrt_render_multi does (same image,
  * same stats); params->rank / world_size / device are ignored and
- * params->bounded_volume_hierarchy must imply the create-time BVH decision. */
+ * params->bounded_volume_hierarchy must imply the create-time BVH decision.
+ * out_rgb may be NULL: the assembled frame then stays in devices[0]'s HBM
+ * (a frame loop that times the GPUs, not the PCIe copy) and zrt_multi_frame
+ * copies it out later. */
 typedef struct zrt_multi zrt_multi;
 int zrt_multi_create(const zrt_scene* scene, const zrt_params* params,
                      const uint32_t* devices, uint32_t n_devices, zrt_multi** out);
 int zrt_multi_render(zrt_multi* multi, const zrt_camera* camera,
                      const zrt_params* params, float* out_rgb, zrt_stats* stats);
 int zrt_multi_destroy(zrt_multi* multi);
+/* The last zrt_multi_render's frame (n_floats = width * height * 3, row 0 =
+ * bottom) copied from devices[0] to out_rgb. */
+int zrt_multi_frame(zrt_multi* multi, float* out_rgb, uint64_t n_floats);
+/* The last zrt_multi_render's render-kernel time of each rank in ms (HIP
+ * events around its launch; n = n_devices of zrt_multi_create). */
+int zrt_multi_rank_ms(zrt_multi* multi, double* kernel_ms, uint32_t n);
 /* Per-scanline counters of the last zrt_multi_render made with
  * ZRT_FLAG_SCANLINES, summed over the ranks (height = params->height). */
 int zrt_multi_scanlines(zrt_multi* multi, zrt_scanline* out, uint32_t height);

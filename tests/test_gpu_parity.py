@@ -748,6 +748,46 @@ def test_trace_grazing_triangles_c5_substitute(scenes):
     assert np.array_equal(p_o, p_ref[:400]) and same_bits(t_o, t_ref[:400]).all()
 
 
+@pytest.mark.parametrize("which", [2, 3, 0, 4])
+def test_trace_grazing_triangles_unguarded_recorded(scenes, which, monkeypatch):
+    """the same grazing-triangle rays traced WITHOUT the guard
+    (ZRT_DEBUG_NO_GUARD: the traversal the default, unguarded render kernels run).
+    The count of rays whose answer differs from the oracle is recorded (printed;
+    round 3's kernel: teapot 8, teapot + balls 7, Man 1 of 20 000).  What is
+    asserted is the tolerance the unguarded default claims: a flip changes one
+    sample of one pixel, and such rays are at most 1 in 1000 of this deliberately
+    adversarial set; the guarded traversal (the test above) has none."""
+    import grazing_tris as G
+    s = scenes(which)
+    pr = prim_array(s.view.contents)
+    mins, maxs, left, right, _ = O.bvh_build(s.view)
+    o, d = G.grazing_triangle_rays(pr, mins, maxs, left, right, n=20000, seed=1, span=G.scene_span(pr))
+    monkeypatch.setenv("ZRT_DEBUG_NO_GUARD", "1")
+    _, bad = _trace_all(s.view, o, d, keep=s)
+    print(f"\nscene {which}: unguarded rays differing from the oracle, per traversal: {bad}")
+    assert bad.get(z.ZRT_TRAVERSAL_REFERENCE, 0) == 0  # (the reference's own traversal has no guard to lose)
+    assert all(v <= 20 for v in bad.values()), bad
+
+
+@pytest.mark.parametrize("scene_index,dims", [(4, (128, 128, 8)), (6, (96, 96, 8))], ids=["teapot-balls", "c5-mesh"])
+def test_unguarded_render_equals_reference_traversal(scenes, scene_index, dims):
+    """the default (unguarded) FAST render on the meshes the
+    guard exists for - scene 4 (teapot + ring of spheres) and scene 6 (the 1.6 M
+    triangle C5 mesh, path-pool loop) - against the REFERENCE traversal (the
+    reference's left-first DFS with its loose slab test, bvh.zig:187-205) on the
+    same frame, > 10^5 rays at depth 20: bit-identical, counters included."""
+    s = scenes(scene_index)
+    w, h, spp = dims
+    fast_img, fast_st = z.render(s, s.camera, z.RenderParams(w, h, spp, 20))
+    ref_img, ref_st = z.render(s, s.camera, z.RenderParams(w, h, spp, 20, traversal=z.ZRT_TRAVERSAL_REFERENCE))
+    assert ref_st["rays_processed"] > 100_000
+    assert fast_st["guard"] == 0.0
+    diff = int((~(fast_img.view(np.uint32) == ref_img.view(np.uint32))).any(axis=2).sum())
+    assert diff == 0, f"{diff} pixels differ from the REFERENCE traversal's frame"
+    for k in COUNTERS:
+        assert fast_st[k] == ref_st[k], k
+
+
 @pytest.mark.parametrize("scene_index", [3, 4])
 def test_render_with_grazing_guard_bit_exact(scenes, scene_index):
     """ZRT_FLAG_GUARD: the render carries the grazing-triangle guard (in the

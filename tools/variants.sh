@@ -1,12 +1,17 @@
 #!/bin/bash
 # Build kernel variants (compile-time knobs) into abvar/<name>/libzrt.so for an
-# A/B session (tools/ab.sh, tools/gpu_ab2.sh).  abvar/ is git-ignored and NOT
-# gpurun-ignored, so the variants travel to the GPU box only while they exist:
-# many are deliberately inexact (A/B probes), so remove them after the session
+# A/B session (tools/ab.sh, tools/gpu_ab2.sh).  abvar/ is git-ignored, and
+# gpurun-ignored (./abvar in .gpurunignore) except while variants exist: building
+# them lifts that line so they travel to the GPU box for the A/B session; --clean
+# removes them (many are deliberately inexact A/B probes) and restores the line
 #   bash tools/variants.sh --clean
 # usage: bash tools/variants.sh name1="-DFOO=1" name2="-DBAR=2" ...
 R=$(cd "$(dirname "$0")/.." && pwd)
-if [ "$1" == "--clean" ]; then rm -rf "$R/abvar"; echo "removed abvar/"; exit 0; fi
+if [ "$1" == "--clean" ]; then
+  rm -rf "$R/abvar"; grep -qx './abvar' $R/.gpurunignore || echo './abvar' >> $R/.gpurunignore
+  echo "removed abvar/ (gpurun-ignored again)"; exit 0
+fi
+sed -i '/^\.\/abvar$/d' $R/.gpurunignore
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   mkdir -p $R/abvar/$name

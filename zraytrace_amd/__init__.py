@@ -202,14 +202,31 @@ class MultiContext:
         devs = (C.c_uint32 * len(devices))(*devices)
         check(lib().zrt_multi_create(view, C.byref(p), devs, len(devices), C.byref(h)))
         self._h = h
+        self.n_ranks = len(devices)
+        self._shape = None
 
-    def render(self, camera, params: RenderParams):
-        out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+    def render(self, camera, params: RenderParams, copy_out: bool = True):
+        """One frame.  copy_out=False leaves it on devices[0] (read it with frame()):
+        returns (None, stats)."""
         st = _ffi.Stats()
         p = params.abi()
-        check(lib().zrt_multi_render(self._h, C.byref(camera), C.byref(p),
-                                     out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+        out = np.zeros((params.height, params.width, 3), dtype=np.float32) if copy_out else None
+        ptr = out.ctypes.data_as(C.POINTER(C.c_float)) if copy_out else None
+        check(lib().zrt_multi_render(self._h, C.byref(camera), C.byref(p), ptr, C.byref(st)))
+        self._shape = (params.height, params.width, 3)
         return out, st.as_dict()
+
+    def frame(self) -> np.ndarray:
+        """The last frame, copied from devices[0] (zrt_multi_frame)."""
+        out = np.zeros(self._shape, dtype=np.float32)
+        check(lib().zrt_multi_frame(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size))
+        return out
+
+    def rank_ms(self) -> list:
+        """Each rank's render-kernel time of the last frame, ms (zrt_multi_rank_ms)."""
+        out = (C.c_double * self.n_ranks)()
+        check(lib().zrt_multi_rank_ms(self._h, out, self.n_ranks))
+        return list(out)
 
     def scanlines(self, height: int) -> np.ndarray:
         """Per-scanline counters of the last render made with ZRT_FLAG_SCANLINES, summed over ranks."""

@@ -131,6 +131,8 @@ SIGNATURES = [
                                    C.POINTER(Stats)]),
     ("zrt_multi_destroy", C.c_int, [_P]),
     ("zrt_multi_scanlines", C.c_int, [_P, C.POINTER(Scanline), C.c_uint32]),
+    ("zrt_multi_frame", C.c_int, [_P, C.POINTER(C.c_float), C.c_uint64]),
+    ("zrt_multi_rank_ms", C.c_int, [_P, C.POINTER(C.c_double), C.c_uint32]),
     ("zrt_trace", C.c_int, [C.POINTER(Scene), C.POINTER(Params), C.POINTER(C.c_float), C.c_uint32,
                             C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     ("zrt_camera_init", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -205,15 +207,27 @@ def load(path: str = LIB_PATH):
             f"{path} is missing: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()'); there is no fallback path")
     lib = C.CDLL(path)
+    in_tree = path == os.path.join(HERE, "libzrt.so")
+    rebuild = "rebuild it (python -c 'import __graft_entry__ as g; g.build()')"
+    # the ABI version first (every version exports zrt_abi_version): the struct
+    # layouts below are this version's, so another version is refused before any
+    # symbol is bound (an A/B variant under ZRT_LIB is warned about, not refused)
+    lib.zrt_abi_version.restype = C.c_int
+    lib.zrt_abi_version.argtypes = []
+    abi = lib.zrt_abi_version()
+    if abi != ABI_VERSION:
+        if in_tree:
+            raise ImportError(f"{path} has ABI version {abi}, this binding expects {ABI_VERSION}: {rebuild}")
+        import warnings
+        warnings.warn(f"ZRT_LIB {path} has ABI version {abi}, this binding expects {ABI_VERSION}")
     for name, restype, argtypes in SIGNATURES:
-        if path != os.path.join(HERE, "libzrt.so") and not hasattr(lib, name):
+        if not hasattr(lib, name):
+            if in_tree:
+                raise ImportError(f"{path} does not export {name} (built from older sources): {rebuild}")
             continue  # an older A/B build variant (ZRT_LIB) may lack newer entry points
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
-    if path == os.path.join(HERE, "libzrt.so") and lib.zrt_abi_version() != ABI_VERSION:
-        raise ImportError(f"{path} has ABI version {lib.zrt_abi_version()}, this binding expects {ABI_VERSION}: "
-                          "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
     if path == LIB_PATH:
         _lib = lib
     return lib

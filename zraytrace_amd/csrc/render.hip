@@ -3924,6 +3924,8 @@ struct zrt_multi {
   std::vector<std::unique_ptr<zrt_ctx, zrt::CtxDeleter>> ctx;
   std::vector<zrt::DevBuf<float>> send;
   zrt::DevBuf<float> gathered, frame;  // on devices[0]
+  size_t frame_n = 0;                  // floats of the last frame in `frame` (0: none rendered yet)
+  std::vector<double> rank_ms;         // the last frame: each rank's render-kernel time (HIP events)
   zrt::Comms comms;
 };
 
@@ -3988,7 +3990,14 @@ int zrt_ctx_create(const zrt_scene* scene, const zrt_params* params, zrt_ctx** o
     // GPU builds the reference BVH only when one is visible
     const bool use_bvh = params->bounded_volume_hierarchy != 0 && scene->n_prims > 10;
     int n_dev = 0;
-    const bool have_dev = hipGetDeviceCount(&n_dev) == hipSuccess && int(params->device) < n_dev;
+    const bool gpus = hipGetDeviceCount(&n_dev) == hipSuccess && n_dev > 0;
+    // with GPUs present, an unusable device is refused before the (seconds-long on a
+    // million-triangle mesh) scene build; without any, the layout check still runs first
+    if (gpus) {
+      rc = zrt::check_device(int(params->device));
+      if (rc) return rc;
+    }
+    const bool have_dev = gpus && int(params->device) < n_dev;
     zrt::HostScene h;
     zrt::flatten_scene(&h, scene, use_bvh, have_dev ? int(params->device) : -1);
     rc = zrt::check_device(int(params->device));
@@ -4546,7 +4555,7 @@ int zrt_multi_destroy(zrt_multi* m) {
 
 int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* params, float* out_rgb,
                      zrt_stats* stats) {
-  if (!m || !camera || !out_rgb) return fail(ZRT_E_INVALID, "null argument");
+  if (!m || !camera) return fail(ZRT_E_INVALID, "null argument");  // out_rgb NULL: the frame stays on devices[0]
   int rc = zrt::validate_params(params);
   if (rc) return rc;
   const uint32_t n = uint32_t(m->ctx.size());
@@ -4578,6 +4587,8 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
     std::memset(&sum, 0, sizeof(sum));
     int device_rc = ZRT_OK;
     std::string device_msg;
+    m->frame_n = 0;
+    m->rank_ms.assign(n, 0.0);
     for (uint32_t r = 0; r < n; ++r) {
       zrt_stats s;
       rc = zrt_ctx_stats(m->ctx[r].get(), &s);  // waits for rank r's launch
@@ -4586,6 +4597,12 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
         device_msg = zrt_last_error();
       }
       else if (rc) return rc;
+      {  // the render kernel alone (ev0 -> ev1; render_ms also holds the schedule probe)
+        float ms = 0.0f;
+        HIPCHK(hipSetDevice(m->ctx[r]->device));
+        HIPCHK(hipEventElapsedTime(&ms, m->ctx[r]->ev0, m->ctx[r]->ev1));
+        m->rank_ms[r] = ms;
+      }
       if (r == 0) {
         sum = s;
         continue;
@@ -4641,13 +4658,34 @@ int zrt_multi_render(zrt_multi* m, const zrt_camera* camera, const zrt_params* p
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(root->stream));
     sum.gather_ms = zrt::now_ms() - t0;
-    HIPCHK(hipMemcpy(out_rgb, m->frame.p, sizeof(float) * frame_n, hipMemcpyDeviceToHost));
+    m->frame_n = frame_n;
+    if (out_rgb) HIPCHK(hipMemcpy(out_rgb, m->frame.p, sizeof(float) * frame_n, hipMemcpyDeviceToHost));
     sum.n_gpus = m->n_distinct;
     if (stats) *stats = sum;
     if (device_rc) return fail(device_rc, device_msg);
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
+}
+
+int zrt_multi_frame(zrt_multi* m, float* out_rgb, uint64_t n_floats) {
+  if (!m || !out_rgb) return fail(ZRT_E_INVALID, "null argument");
+  if (m->frame_n == 0) return fail(ZRT_E_INVALID, "no frame: zrt_multi_frame before a successful zrt_multi_render");
+  if (n_floats != m->frame_n) return fail(ZRT_E_INVALID, "n_floats differs from the last frame's width * height * 3");
+  try {
+    HIPCHK(hipSetDevice(m->ctx[0]->device));
+    HIPCHK(hipMemcpy(out_rgb, m->frame.p, sizeof(float) * m->frame_n, hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_multi_rank_ms(zrt_multi* m, double* kernel_ms, uint32_t n) {
+  if (!m || !kernel_ms) return fail(ZRT_E_INVALID, "null argument");
+  if (m->rank_ms.empty()) return fail(ZRT_E_INVALID, "no frame rendered yet");
+  if (n != m->rank_ms.size()) return fail(ZRT_E_INVALID, "n differs from the context's rank count");
+  for (uint32_t r = 0; r < n; ++r) kernel_ms[r] = m->rank_ms[r];
+  return ZRT_OK;
 }
 
 int zrt_multi_scanlines(zrt_multi* m, zrt_scanline* out, uint32_t height) {
@@ -4737,7 +4775,9 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.layout = c->layout;
     a.graze_m = c->graze_m;
     a.graze_leaf = c->graze_leaf;
-    a.guard = c->guard;
+    // tests: ZRT_DEBUG_NO_GUARD=1 traces without the grazing-triangle guard (the
+    // default render kernels' traversal), to record what the guard is for
+    a.guard = std::getenv("ZRT_DEBUG_NO_GUARD") ? 0.0f : c->guard;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
     a.n_top = c->n_top;
