@@ -107,6 +107,7 @@ struct KArgs {
   uint32_t wf_thresh;  // wavefront loop: shade when ready lanes >= this / 64 of the unit's active lanes
                        // (path-pool loop: once the queue is empty and fewer than 64 - this lanes traverse)
   uint32_t lds_pool_off;  // path-pool loop: rays, hits and queues (kBlockPaths paths per block)
+  uint32_t lds_state_off;  // lockstep FAST loop: lane state across the traversal, [word][lane] u32 (LaneState)
   uint32_t n_paths;       //   paths of the launch (grid x kBlockPaths): the stride of its global attenuation rows
   uint32_t tri_rcp_fast;  // every triangle |n| < 2^125: 1/det by dev::rcp_core (RayT::rcp_det)
   float scene_extent;     // the triangles' largest |coordinate| (ray_slack)
@@ -168,10 +169,6 @@ __device__ __forceinline__ uint64_t prof_stamp() {
 }
 
 constexpr int kBlock = 256;
-#ifndef ZRT_STACK_LDS_BYTES
-#define ZRT_STACK_LDS_BYTES (28 * 1024)  // FAST traversal stack in LDS per block (5 blocks / CU fit)
-#endif
-constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #ifndef ZRT_PROBE_SPP
 #define ZRT_PROBE_SPP 1  // samples per pixel of the scheduling probe; A/B at N=8: 1, 2, 4, 8 give the same render launch
 #endif
@@ -192,6 +189,12 @@ constexpr size_t kStackLdsBytes = ZRT_STACK_LDS_BYTES;
 #endif
 #ifndef ZRT_LDS_TOP
 #define ZRT_LDS_TOP 1  // FAST: the wide tree's top levels read from LDS (0: A/B, every node from global memory)
+#endif
+#ifndef ZRT_LANE_LDS
+#define ZRT_LANE_LDS 1  // lockstep FAST loop: RNG state, chunk sums, sample and depth kept in LDS across the traversal
+#endif
+#ifndef ZRT_STACK_ROWS_LOCK
+#define ZRT_STACK_ROWS_LOCK 16  // lockstep FAST loop: traversal stack rows in LDS (deeper rows in global memory)
 #endif
 #ifndef ZRT_SYNC_SAMPLES
 #define ZRT_SYNC_SAMPLES 1  // the lanes of a wave wait for each other every this many samples
@@ -1108,23 +1111,42 @@ struct WideNode {
   float4 nx, ny, nz, fx, fy, fz, ra;
 };
 
-__device__ __forceinline__ void wide_load(const float4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
+// The top wide nodes in LDS are read through an LDS-typed (32-bit) pointer of
+// native 4-vectors (one ds_read_b128 each): a traversal's current node is kept
+// as an index and addressed per use, never as a 64-bit generic pointer that
+// would select between LDS and global memory at every read (and cost a VGPR
+// pair across the whole loop).
+typedef float nf4 __attribute__((ext_vector_type(4)));
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(3))) nf4 lds_cnf4;
+#else
+typedef const nf4 lds_cnf4;
+#endif
+__device__ __forceinline__ float4 f4(nf4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+
+__device__ __forceinline__ void wide_set(float4 m0, float4 m1, float4 m2, float4 m3, float4 m4, float4 m5, float4 m6,
+                                         bool sx, bool sy, bool sz, WideNode& w) {
 #if ZRT_OCT_COPIES
   (void)sx; (void)sy; (void)sz;
-  w.nx = q[0]; w.ny = q[1]; w.nz = q[2]; w.fx = q[3]; w.fy = q[4]; w.fz = q[5]; w.ra = q[6];
+  w.nx = m0; w.ny = m1; w.nz = m2; w.fx = m3; w.fy = m4; w.fz = m5;
 #else
-  const float4 m0 = q[0], m1 = q[1], m2 = q[2], m3 = q[3], m4 = q[4], m5 = q[5];
   w.nx = sx ? m3 : m0; w.fx = sx ? m0 : m3;
   w.ny = sy ? m4 : m1; w.fy = sy ? m1 : m4;
   w.nz = sz ? m5 : m2; w.fz = sz ? m2 : m5;
-  w.ra = q[6];
 #endif
+  w.ra = m6;
+}
+__device__ __forceinline__ void wide_load(const float4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
+  wide_set(q[0], q[1], q[2], q[3], q[4], q[5], q[6], sx, sy, sz, w);
+}
+__device__ __forceinline__ void wide_load(lds_cnf4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
+  wide_set(f4(q[0]), f4(q[1]), f4(q[2]), f4(q[3]), f4(q[4]), f4(q[5]), f4(q[6]), sx, sy, sz, w);
 }
 
 // Where a ray reads the wide tree: its octant's copy (global memory) and that
 // copy's top levels in LDS.
 struct WideView {
-  const float4* __restrict__ top;  // this octant's copy of the top nodes in LDS
+  lds_cnf4* __restrict__ top;      // this octant's copy of the top nodes in LDS
   uint32_t base;                   // float4 offset of this octant's copy (< 2^32)
   uint32_t n_top;
   bool sx, sy, sz;
@@ -1142,15 +1164,24 @@ __device__ __forceinline__ WideView wide_view(const KArgs& a, const RayT& r, con
   const uint32_t oct = 0;
   v.base = 0;
 #endif
-  v.top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
+  v.top = (lds_cnf4*)(lds_top) + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
   v.n_top = ZRT_LDS_TOP ? a.n_top : 0u;
   return v;
 }
 
 // The address of wide node `i` for this ray: LDS for a top-level node, else
-// its octant copy in global memory.
+// its octant copy in global memory (a generic pointer: the rare per-axis tests)
 __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const WideView& v, uint32_t i) {
-  return i < v.n_top ? v.top + 8u * i : a.wnodes + (v.base + 8u * i);
+  return i < v.n_top ? (const float4*)(v.top + 8u * i) : a.wnodes + (v.base + 8u * i);
+}
+// wide node i into w: LDS for a top-level node, else global memory
+__device__ __forceinline__ void wide_load_at(const KArgs& a, const WideView& v, uint32_t i, WideNode& w) {
+  if (i < v.n_top) wide_load(v.top + 8u * i, v.sx, v.sy, v.sz, w);
+  else wide_load(a.wnodes + (v.base + 8u * i), v.sx, v.sy, v.sz, w);
+}
+// float4 j of wide node i
+__device__ __forceinline__ float4 wide_f4(const KArgs& a, const WideView& v, uint32_t i, uint32_t j) {
+  return i < v.n_top ? f4(v.top[8u * i + j]) : a.wnodes[v.base + 8u * i + j];
 }
 
 // FAST: near-first over the 4-wide tree (accel_build.cpp), stored once per
@@ -1168,20 +1199,19 @@ __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const Wid
 // (pushing the farther inner children), intersects the opened leaves and loads
 // the next node into `w` / q.  Returns false when the traversal is over (then
 // the order-hazard test of wide_finish follows).  Its state between calls is
-// (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
+// (w, qn, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
 template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK, bool GUARD = true>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
-                                          const float4*& q, uint32_t& sp, float& best_t, int& best,
+                                          uint32_t& qn, uint32_t& sp, float& best_t, int& best,
                                           uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
                                           Coh& coh) {
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;  // rows allocated: the deepest push + 3
-  // the first rows in LDS, the rest in global memory (32-bit stacks only: the
-  // host gives a 16-bit stack that does not fit in LDS a 32-bit one)
-  constexpr bool kOvf = sizeof(StackT) == 4;
-  const uint32_t rows = kOvf ? a.lds_rows : cap;
+  // the first rows in LDS, the rest in global memory (a.lds_rows: zrt::plan_lds)
+  constexpr bool kOvf = true;
+  const uint32_t rows = a.lds_rows;
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float inf = __builtin_inff();
   const bool sx = v.sx, sy = v.sy, sz = v.sz;
@@ -1286,6 +1316,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool w0 = o0 && (pg || !ZRT_SURE(s0)), w1 = o1 && (pg || !ZRT_SURE(s1));
   const bool w2 = o2 && (pg || !ZRT_SURE(s2)), w3 = o3 && (pg || !ZRT_SURE(s3));
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
+    const float4* q = wide_node_ptr(a, v, qn);
     if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en, gg);
     if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en, gg);
     if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz, s2.en, gg);
@@ -1312,7 +1343,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if (r##K < -kSphereSlotBias) {                                                                             \
     o##K = !pw && !deg && ZRT_SURE(s##K);                                                                    \
     if (!o##K && !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, Eg) > 0.001f)          \
-      o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);                                                   \
+      o##K = static_ok_slot(wide_node_ptr(a, v, qn), K, r, sx, sy, sz, s##K.en);                             \
     r##K += kSphereSlotBias;                                                                                 \
   }
     ZRT_SPHERE_SLOT(0)
@@ -1324,7 +1355,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #endif
 #undef ZRT_SURE
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
-  const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
+  const uint32_t leaf_n = qn;  // (the leaves are intersected after the next node is chosen)
   int32_t next = -1;
   // inner slots that pass, keyed by entry distance
   float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
@@ -1390,7 +1421,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
     uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
     if (open != 0) {
-      const float4 rb = leaf_q[7];
+      const float4 rb = wide_f4(a, v, leaf_n, 7);
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(open);
         open &= open - 1u;
@@ -1417,7 +1448,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
       } while (open != 0);
     }
   } else if ((l0 | l1 | l2 | l3) != 0) {
-    const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
+    const float4 rb = wide_f4(a, v, leaf_n, 7);  // (loaded with the node instead: 3.6 % slower, 2 spills)
 #define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
   if (L != 0) {                                                                                     \
     const int pb = as_int(RB);                                                                      \
@@ -1438,14 +1469,12 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     coh.unodes += uni ? 1u : 0u;
   }
   if (next < 0) return false;
+  qn = (uint32_t)next;
   if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS (ds_read)
-    const float4* __restrict__ t = v.top + 8u * (uint32_t)next;
-    q = t;
-    wide_load(t, sx, sy, sz, w);
+    wide_load(v.top + 8u * (uint32_t)next, sx, sy, sz, w);
   } else {
     const uint32_t at = v.base + 8u * (uint32_t)next;  // this ray's octant copy
     const float4* __restrict__ g = a.wnodes + at;
-    q = g;
     const uint32_t fa = __builtin_amdgcn_readfirstlane(at);
     if (SCALAR_NODES && __ballot(at != fa) == 0ull) {  // one node in every active lane: scalar loads
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1499,10 +1528,10 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const WideView v = wide_view(a, r, lds_top);
   uint32_t sp = 0;
   // the root is node 0 of this octant's copy (in LDS when the top levels are)
-  const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+  uint32_t qn = 0;
   WideNode w;
-  wide_load(q, v.sx, v.sy, v.sz, w);
-  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves,
+  wide_load_at(a, v, 0u, w);
+  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves,
                                                            c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
@@ -1652,6 +1681,24 @@ __device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ 
     if (d) atomicAdd(&rows[3 * py + 0], (unsigned long long)d);
     if (r) atomicAdd(&rows[3 * py + 1], (unsigned long long)r);
     if (b) atomicAdd(&rows[3 * py + 2], (unsigned long long)b);
+  }
+}
+
+// ZRT_FLAG_SCANLINES for a wave whose events are ballot masks (lane p = pixel p of
+// the 8x8 tile whose bottom row is y0): each tile row's count added to its frame
+// row by lane 0.  Called with the whole wave converged.
+__device__ __forceinline__ void scanline_masks(unsigned long long* __restrict__ rows, uint32_t y0, uint32_t height,
+                                               uint64_t md, uint64_t mr, uint64_t mb) {
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t py = y0 + k;
+    const uint32_t d = __popcll((md >> (8 * k)) & 0xffull), r = __popcll((mr >> (8 * k)) & 0xffull);
+    const uint32_t b = __popcll((mb >> (8 * k)) & 0xffull);
+    if (py < height && (d | r | b) && __lane_id() == 0) {
+      if (d) atomicAdd(&rows[3 * py + 0], (unsigned long long)d);
+      if (r) atomicAdd(&rows[3 * py + 1], (unsigned long long)r);
+      if (b) atomicAdd(&rows[3 * py + 2], (unsigned long long)b);
+    }
   }
 }
 
@@ -1854,6 +1901,41 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
   }
 }
 
+// The lockstep loop's lane state parked in LDS across a traversal: the RNG
+// state's words, then the chunk sums (r, g, b), the sample and the depth left,
+// each a [word][lane] row of u32 (consecutive lanes, consecutive banks).  The
+// traversal writes the stack rows of the same LDS, so the compiler cannot keep
+// the values in registers past the traversal: they are stored and re-read.
+template <int PRNG>
+struct LaneState {
+  static constexpr uint32_t kRngWords = sizeof(Rng<PRNG>) / 4;
+  static constexpr uint32_t kWords = kRngWords + 5;
+  __device__ __forceinline__ static void park(lds_u32* p, const Rng<PRNG>& rng, float r, float g, float b,
+                                              uint32_t sample, uint32_t depth) {
+    uint32_t w[kRngWords];
+    __builtin_memcpy(w, &rng, sizeof(w));
+#pragma unroll
+    for (uint32_t k = 0; k < kRngWords; ++k) p[k * kBlock] = w[k];
+    p[(kRngWords + 0) * kBlock] = __float_as_uint(r);
+    p[(kRngWords + 1) * kBlock] = __float_as_uint(g);
+    p[(kRngWords + 2) * kBlock] = __float_as_uint(b);
+    p[(kRngWords + 3) * kBlock] = sample;
+    p[(kRngWords + 4) * kBlock] = depth;
+  }
+  __device__ __forceinline__ static void unpark(const lds_u32* p, Rng<PRNG>& rng, float& r, float& g, float& b,
+                                                uint32_t& sample, uint32_t& depth) {
+    uint32_t w[kRngWords];
+#pragma unroll
+    for (uint32_t k = 0; k < kRngWords; ++k) w[k] = p[k * kBlock];
+    __builtin_memcpy(&rng, w, sizeof(w));
+    r = __uint_as_float(p[(kRngWords + 0) * kBlock]);
+    g = __uint_as_float(p[(kRngWords + 1) * kBlock]);
+    b = __uint_as_float(p[(kRngWords + 2) * kBlock]);
+    sample = p[(kRngWords + 3) * kBlock];
+    depth = p[(kRngWords + 4) * kBlock];
+  }
+};
+
 // StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
 // more blocks fit per CU), uint32_t otherwise.
 template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
@@ -1872,6 +1954,12 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   }
   const int lane = (int)__lane_id();
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;  // n_lanes < 2^32
+  // FAST: what a lane carries across its traversal - RNG state, chunk sums, sample,
+  // depth - is parked in LDS ([word][lane], LaneState) while it traverses: the
+  // traversal needs every VGPR of the 6-wave budget, and these values otherwise
+  // went to scratch (9 stores + 9 loads per step through the vector-memory path)
+  constexpr bool kLaneLds = MODE == 3 && ZRT_LANE_LDS;
+  lds_u32* st_l = (lds_u32*)(lds_raw + a.lds_state_off) + threadIdx.x;
 
   bool active = false, in_sample = false;  // active: this lane still has samples in the wave's unit
   uint32_t sample = 0;
@@ -1885,7 +1973,11 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   uint32_t depth_left = 0;  // attenuations stacked so far: max_depth - depth_left
   Rng<PRNG> rng;
   rng.init(0);
-  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
+  // raytrace.zig:20-34's Progress counters of the current unit, wave-uniform (SGPRs):
+  // each step's events are ballots taken where the wave is converged, so no lane
+  // carries a counter across the traversal (three fewer long-lived VGPRs)
+  uint32_t s_depth = 0, s_refl = 0, s_bg = 0;
+  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
   ExcessAcc excess;  // REFERENCE traversal, STATS flavour only
@@ -1916,10 +2008,12 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         if (cur_lt != 0xffffffffu)  // the finished unit's chunk sums, [chunk][pixel slot]: one 1 KiB store per wave
           a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
         if (a.unit_cost && cur_lt != 0xffffffffu && lane == 0) a.unit_cost[cur_lt] = iters;
-        if (a.scanlines && cur_lt != 0xffffffffu) {  // the finished unit's counters, per frame row
-          flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
-          c_depth = c_refl = c_bg = 0;  // (so the launch totals are the rows' sums)
+        if ((s_depth | s_refl | s_bg) != 0u && lane == 0) {  // the finished unit's Progress counters
+          if (s_depth) atomicAdd(&a.counters[kDepthHits], (unsigned long long)s_depth);
+          if (s_refl) atomicAdd(&a.counters[kReflections], (unsigned long long)s_refl);
+          if (s_bg) atomicAdd(&a.counters[kBackground], (unsigned long long)s_bg);
         }
+        s_depth = s_refl = s_bg = 0;
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.work_counter, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
@@ -1948,8 +2042,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       c_loops += lane == 0 ? 1u : 0u;
       c_lsteps += runnable ? 1u : 0u;
     }
-    if (!runnable) continue;
-
+    uint32_t e_depth = 0, e_refl = 0, e_bg = 0;  // this step's events in this lane
+    if (runnable) {
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
     if (!in_sample) {
       const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
@@ -1971,7 +2065,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     bool path_end = false, sky = false;
     V3 L = mk(0.0f, 0.0f, 0.0f);
     if (depth_left == 0) {
-      ++c_depth;
+      ++e_depth;
       path_end = true;
     } else {
       if (STATS) ++c_rays;
@@ -2006,13 +2100,15 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
+        if (kLaneLds) LaneState<PRNG>::park(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
         traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
+        if (kLaneLds) LaneState<PRNG>::unpark(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph, &excess);
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
       shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
-                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
+                        sky, L, e_bg, e_refl, c_shade, c_tex, coh);
     }
 
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
@@ -2027,6 +2123,14 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       if (++sample == unit_end) active = false;  // chunk done: its sequential sum, stored when the unit ends
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
+    }  // runnable
+    {  // the wave is converged again: its step's events as ballots
+      const uint64_t md = __ballot(e_depth != 0u), mr = __ballot(e_refl != 0u), mb = __ballot(e_bg != 0u);
+      s_depth += (uint32_t)__popcll(md);
+      s_refl += (uint32_t)__popcll(mr);
+      s_bg += (uint32_t)__popcll(mb);
+      if (a.scanlines) scanline_masks(a.scanlines, y0, a.height, md, mr, mb);
+    }
   }
   if (ZRT_PROFILE && lane == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(&a.counters[kProfSlot + k], (unsigned long long)pf[k]);
@@ -2037,9 +2141,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     }
   }
 
-  wave_add_u64(&a.counters[kDepthHits], c_depth);
-  wave_add_u64(&a.counters[kReflections], c_refl);
-  wave_add_u64(&a.counters[kBackground], c_bg);
+  // (the loop leaves when the counter is exhausted, after flushing its last unit)
   if (STATS) {
     wave_add_u64(&a.counters[kRays], c_rays);
     wave_add_u64(&a.counters[kNodes], c_nodes);
@@ -2127,7 +2229,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
-  const float4* q = nullptr;  // the lane's current node (LDS or global)
+  uint32_t qn = 0;  // the lane's current node (LDS or global)
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
@@ -2142,12 +2244,12 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       WideNode w;
       if (trav) {
         v = wide_view(a, r, lds_top);
-        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
+        wide_load_at(a, v, qn, w);  // the suspended node (re)loaded
       }
       for (;;) {
         if (trav) {
           // (its lanes' nodes are rarely one: no scalar-load test, C5 -1.4 % with it)
-          if (!wide_iter<STATS, StackT, false, true, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, false, true, false>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             trav = false;
@@ -2236,10 +2338,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
         best_t = __builtin_inff();
     best = -1;
     sp = 0;
-    {
-      const WideView v = wide_view(a, r, lds_top);
-      q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
-    }
+    qn = 0;  // the root of the ray's octant copy
     trav = true;
   }
 
@@ -2379,7 +2478,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
-  const float4* q = nullptr;
+  uint32_t qn = 0;  // the lane's current node
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
   uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0;
@@ -2393,7 +2492,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
       WideNode w;
       if (trav) {
         v = wide_view(a, r, lds_top);
-        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
+        wide_load_at(a, v, qn, w);  // the suspended node (re)loaded
       }
       for (;;) {
         const uint64_t idle = __ballot(!trav);
@@ -2414,15 +2513,15 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
             best = -1;
             sp = 0;
             v = wide_view(a, r, lds_top);
-            q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
-            wide_load(q, v.sx, v.sy, v.sz, w);
+            qn = 0;  // the root of the ray's octant copy
+            wide_load_at(a, v, 0u, w);
             trav = true;
           }
           const uint32_t n_idle = (uint32_t)__builtin_popcountll(idle);
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
@@ -2779,7 +2878,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 #define ZRT_ATT_ROWS_LIST 24  // list loops (MODE 0 / 6): attenuation rows kept in LDS (as many as their 6-block share holds)
 #endif
 #ifndef ZRT_ATT_ROWS_LOCK
-#define ZRT_ATT_ROWS_LOCK 6  // lockstep FAST loop: attenuation rows kept in LDS (6 KiB per block, as 2 rows of 3 floats were)
+#define ZRT_ATT_ROWS_LOCK 4  // lockstep FAST loop: attenuation rows kept in LDS (4 KiB per block, beside its lane state)
 #endif
 #ifndef ZRT_ATT_ROWS_WF
 #define ZRT_ATT_ROWS_WF 12  // wavefront loop: attenuation rows kept in LDS (12 KiB per block, as 4 rows of 3 floats were)
@@ -3678,6 +3777,11 @@ void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 7) return stk16 ? kernel_ptr<7, PRNG, STATS, uint16_t>() : kernel_ptr<7, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
+#ifdef ZRT_ISA_KERNEL
+// tools/isa.sh: device assembly of ONE render kernel (register / spill probes in
+// seconds instead of minutes); ZRT_ISA_KERNEL = MODE, PRNG, STATS, StackT
+void* select_kernel(int, uint32_t, bool, bool) { return kernel_ptr<ZRT_ISA_KERNEL>(); }
+#else
 void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
   if (prng == ZRT_PRNG_XOSHIRO256)
     return stats ? select_kernel_ps<ZRT_PRNG_XOSHIRO256, true>(mode, stk16)
@@ -3685,11 +3789,17 @@ void* select_kernel(int mode, uint32_t prng, bool stats, bool stk16) {
   return stats ? select_kernel_ps<ZRT_PRNG_XOROSHIRO128, true>(mode, stk16)
                : select_kernel_ps<ZRT_PRNG_XOROSHIRO128, false>(mode, stk16);
 }
+#endif
 
 template <int PRNG>
 void* probe_ptr(bool stk16) {
+#ifdef ZRT_ISA_KERNEL
+  (void)stk16;
+  return nullptr;
+#else
   return stk16 ? reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint16_t>)
                : reinterpret_cast<void*>(&schedule_probe_kernel<PRNG, uint32_t>);
+#endif
 }
 
 // The block's dynamic LDS: [stack rows][lane] (StackT), then (FAST) the top
@@ -3698,12 +3808,40 @@ void* probe_ptr(bool stk16) {
 // (its __launch_bounds__) still fit: 160 KiB / that many blocks per CU.
 struct LdsPlan {
   uint32_t stack_rows = 0, top_off = 0, att_off = 0, att_rows = 0, mat_off = 0, mats_in_lds = 0, pool_off = 0;
-  size_t bytes = 0;
+  uint32_t state_off = 0;
+  size_t bytes = 0, budget = 0;
+  size_t stack_b = 0, top_b = 0, pool_b = 0, state_b = 0, att_b = 0, mats_b = 0;  // region sizes (check_plan)
 };
+// Every region of a plan inside the block's share and disjoint from the others,
+// float4 regions 16-B aligned (the kernels index them from lds_raw by these
+// offsets, nothing else keeps them apart); a violation is a bug in plan_lds.
+void check_plan(const LdsPlan& L) {
+  struct Reg { size_t off, n; const char* name; bool f4; };
+  const Reg regs[] = {{0, L.stack_b, "stack", false}, {L.top_off, L.top_b, "top nodes", true},
+                      {L.pool_off, L.pool_b, "pool", true}, {L.state_off, L.state_b, "lane state", false},
+                      {L.att_off, L.att_b, "attenuation rows", false}, {L.mat_off, L.mats_b, "materials", true}};
+  for (const Reg& x : regs) {
+    if (!x.n) continue;
+    if (x.off + x.n > L.bytes)
+      throw Error(ZRT_E_UNSUPPORTED, std::string("LDS plan: ") + x.name + " past the plan's end");
+    if (x.f4 && x.off % 16)
+      throw Error(ZRT_E_UNSUPPORTED, std::string("LDS plan: ") + x.name + " not 16-B aligned");
+    for (const Reg& y : regs)
+      if (&x != &y && y.n && x.off < y.off + y.n && y.off < x.off + x.n)
+        throw Error(ZRT_E_UNSUPPORTED, std::string("LDS plan: ") + x.name + " overlaps " + y.name);
+  }
+}
+// 32-bit words of the lockstep loop's lane state (LaneState)
+uint32_t lane_state_words(uint32_t prng) {
+  return (prng == ZRT_PRNG_XOSHIRO256 ? LaneState<ZRT_PRNG_XOSHIRO256>::kWords
+                                      : LaneState<ZRT_PRNG_XOROSHIRO128>::kWords);
+}
 // pool: the path-pool loop (MODE 5): its attenuation rows are per path
-// (kBlockPaths per block), and its rays / hits / queues follow them
-LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf = false,
-                 bool pool = false) {
+// (kBlockPaths per block), and its rays / hits / queues follow them.
+// The lockstep FAST loop (mode 3, neither wf nor pool) also holds its lane state
+// (ZRT_LANE_LDS) and keeps at most ZRT_STACK_ROWS_LOCK stack rows in LDS.
+LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth,
+                 bool wf, bool pool, uint32_t prng) {
   const uint32_t waves = mode == 3 ? (pool ? ZRT_WAVES_POOL : wf ? ZRT_WAVES_WF : ZRT_WAVES_WIDE)
                          : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
   // 256-thread blocks: `waves` blocks per CU; 1 KiB below the even share (a
@@ -3711,8 +3849,10 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   const size_t budget = (160u << 10) / waves - (1u << 10);
   const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
   const size_t row_att = sizeof(uint32_t) * (pool ? kBlockPaths : kBlock);  // one att code per lane / path
-  const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * kOctCopies : 0;
+  const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(n_top) * 8 * sizeof(float4) * kOctCopies : 0;
   const size_t pool_b = pool ? kPoolLdsBytes : 0;
+  const bool lock = mode == 3 && !wf && !pool;
+  const size_t state = lock && ZRT_LANE_LDS ? size_t(lane_state_words(prng)) * sizeof(uint32_t) * kBlock : 0;
   // attenuation rows wanted: rows 0 .. max_depth-2 are ever pushed (raytrace.zig:99 at depth > 1).
   // A row is one 4-B att code per lane (att_code; round 3: three floats, 12 B), so
   // the same LDS holds three times the rows: the lockstep loop 6 (round 3, 2 rows
@@ -3726,32 +3866,52 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   if (const char* e = std::getenv("ZRT_ATT_LDS_ROWS")) want = uint32_t(std::atoi(e));
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
   LdsPlan L;
-  if (mode == 3 && !stk16) {
-    // deep trees: the stack takes what the top nodes and two attenuation rows leave
+  L.budget = budget;
+  if (mode == 3 && (!stk16 || lock)) {
+    // the stack takes what the top nodes, the lane state and the wanted attenuation
+    // rows leave (the lockstep loop: at most ZRT_STACK_ROWS_LOCK rows; it wants
+    // ZRT_ATT_ROWS_LOCK att rows); deeper rows live in global memory (wide_iter)
     want = std::min<uint32_t>(want, att_cap);
-    const size_t room = budget > top + pool_b + want * row_att ? budget - top - pool_b - want * row_att : 0;
+    const size_t fixed = top + pool_b + state + want * row_att;
+    const size_t room = budget > fixed ? budget - fixed : 0;
     L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(stack_depth, uint32_t(room / (kBlock * entry))));
+    if (lock) L.stack_rows = std::min<uint32_t>(L.stack_rows, ZRT_STACK_ROWS_LOCK);
   } else {
-    L.stack_rows = stack_depth;  // the whole stack in LDS (16-bit FAST: it fits kStackLdsBytes)
+    L.stack_rows = stack_depth;  // the whole stack in LDS (the callers check it fits)
   }
   if (const char* f = std::getenv("ZRT_STACK_LDS_ROWS"))  // tests: force the overflow rows into use
     if (mode == 3) L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(L.stack_rows, uint32_t(std::atoi(f))));
   const size_t stack = (size_t(L.stack_rows) * kBlock * entry + 15) & ~size_t(15);
-  const size_t used = stack + top + pool_b;
+  const size_t used = stack + top + pool_b + state;
   L.att_rows = std::min<uint32_t>(want, used < budget ? uint32_t((budget - used) / row_att) : 0u);
   L.top_off = uint32_t(stack);
   L.pool_off = uint32_t(stack + top);
+  L.state_off = uint32_t(stack + top + pool_b);
   L.att_off = uint32_t(used);
   L.bytes = used + L.att_rows * row_att;
+  L.stack_b = size_t(L.stack_rows) * kBlock * entry;
+  L.top_b = top;
+  L.pool_b = pool_b;
+  L.state_b = state;
+  L.att_b = L.att_rows * row_att;
   // the material table, if it fits what is left (ZRT_MATS_LDS=0: A/B, always global)
-  const size_t mats = size_t(c->n_mats) * sizeof(DevMaterial);
+  const size_t mats = size_t(n_mats) * sizeof(DevMaterial);
   const char* me = std::getenv("ZRT_MATS_LDS");
   if (mats > 0 && L.bytes + mats <= budget && !(me && std::atoi(me) == 0)) {
     L.mat_off = uint32_t(L.bytes);
     L.mats_in_lds = 1;
     L.bytes += mats;
+    L.mats_b = mats;
   }
+  // the lockstep FAST kernel's waves per SIMD hold only within the share (the
+  // other loops' plans may exceed it: their launch then fits fewer blocks per CU)
+  if (lock && L.bytes > budget) throw Error(ZRT_E_UNSUPPORTED, "LDS plan: the lockstep loop's regions exceed its share");
+  check_plan(L);
   return L;
+}
+LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf, bool pool,
+                 uint32_t prng) {
+  return plan_lds(c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf, pool, prng);
 }
 
 // Longest-processing-time-first order of this rank's tiles (zrt.h,
@@ -4054,16 +4214,14 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                      : p->traversal == ZRT_TRAVERSAL_REFERENCE ? 2
                      : p->traversal == ZRT_TRAVERSAL_BINARY ? 1 : 3;
     const bool diag = (p->flags & ZRT_FLAG_STATS) != 0;
-    // FAST: a 16-bit stack when node indices fit and the whole stack fits the
-    // LDS budget (else the 32-bit flavour, whose deep rows go to global memory)
+    // FAST: a 16-bit stack when node indices fit (either flavour keeps its first
+    // rows in LDS and deeper ones in global memory, zrt::plan_lds)
     const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
     // (FAST also holds the reference traversal's rows for its order-hazard replay)
     uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
     if (const char* cap = std::getenv("ZRT_DEBUG_STACK_CAP"))  // tests: a stack too small for the tree
       stack_depth = std::max<uint32_t>(4, std::min<uint32_t>(stack_depth, uint32_t(std::atoi(cap))));
-    bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
-                                 size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
-                           : c->n_nodes < 65536;
+    bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows : c->n_nodes < 65536;
     // FAST: the wavefront loop (MODE 4) where lanes' traversal lengths diverge
     const bool wf = mode == 3 && p->max_depth >= 1 && zrt::use_wavefront(c, stk16);
     // the path-pool loop (MODE 5) for the same cases, when asked for; a 16-bit stack
@@ -4086,7 +4244,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool);
+    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
     int per_cu = 0;
@@ -4184,6 +4342,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.att_lds_rows = lp.att_rows;
     a.lds_mat_off = lp.mat_off;
     a.lds_pool_off = lp.pool_off;
+    a.lds_state_off = lp.state_off;
     a.n_paths = uint32_t(n_paths);
     a.n_mats = c->n_mats;
     a.mats_in_lds = lp.mats_in_lds;
@@ -4735,11 +4894,9 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
                      : params->traversal == ZRT_TRAVERSAL_BINARY ? 1 : 3;
     const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
     const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
-    const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows &&
-                                       size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) <= zrt::kStackLdsBytes
-                                 : c->n_nodes < 65536;
+    const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows : c->n_nodes < 65536;
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c.get(), mode, stk16, stack_depth, 0);
+    const zrt::LdsPlan lp = zrt::plan_lds(c.get(), mode, stk16, stack_depth, 0, false, false, ZRT_PRNG_XOROSHIRO128);
     const uint32_t lds_rows = lp.stack_rows;
     const uint32_t grid = (n_rays + zrt::kBlock - 1) / zrt::kBlock;
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
@@ -4791,7 +4948,11 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     void* fn = nullptr;
 #define ZRT_TK(M) (stk16 ? reinterpret_cast<void*>(&zrt::trace_kernel<M, uint16_t>) \
                          : reinterpret_cast<void*>(&zrt::trace_kernel<M, uint32_t>))
+#ifdef ZRT_ISA_KERNEL
+    fn = nullptr;
+#else
     fn = mode == 0 ? ZRT_TK(0) : mode == 1 ? ZRT_TK(1) : mode == 2 ? ZRT_TK(2) : ZRT_TK(3);
+#endif
 #undef ZRT_TK
     const float* rp = d_rays.p;
     float* tp = d_t.p;
