@@ -493,6 +493,15 @@ int zrt_bvh_build_device(const zrt_scene* scene, uint32_t device, zrt_bvh_node**
 int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t n, uint32_t device);
 int zrt_debug_rng(uint32_t prng, uint64_t key, uint64_t* out, uint32_t n, uint32_t device);
 int zrt_debug_division(uint64_t n, uint64_t* counts, uint32_t device);
+/* Host-side check of the kernels' LDS layouts for this scene (no device
+ * needed): the scene is flattened as zrt_ctx_create does, then every plan the
+ * launch code can make - each sampling loop, stack width, PRNG and a range of
+ * max depths - is checked region by region (stack rows, top wide nodes, pool
+ * queues, lane state, attenuation rows, materials: in the block's LDS, disjoint,
+ * float4 regions 16-B aligned; the lockstep loop's plan within its 6-block
+ * share).  n_checked: the number of plans checked.  ZRT_E_UNSUPPORTED names the
+ * first violation. */
+int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked);
 
 #ifdef __cplusplus
 }

@@ -313,3 +313,15 @@ def test_u8_texel_values_by_short_division():
         r = rn32(F(float(a)) - F(float(q)) * F(float(b)))
         got = rn32(F(float(r)) * F(float(y)) + F(float(q)))
         assert np.float32(got).view(np.uint32) == (np.float32(k) / b).view(np.uint32), k
+
+
+@pytest.mark.parametrize("index", [0, 1, 2, 3, 4])
+def test_lds_plans_disjoint(scenes, index):
+    """every LDS layout the launch code plans for the scene -
+    list, binary, reference, lockstep / wavefront / path-pool FAST loops, 16- and
+    32-bit stacks, both PRNGs, max depths 0..50 - keeps its regions (stack rows,
+    top wide nodes, pool queues, the lockstep loop's parked lane state, attenuation
+    rows, materials) disjoint, inside the plan and float4-aligned, and the lockstep
+    plan inside its 6-block share (render.hip check_plan).  No device needed."""
+    n = z.debug_lds_plans(scenes(index))
+    assert n == 4 * 0 + (1 + 1 + 1 + 3) * 2 * 2 * 6  # modes 0-2 one loop each, mode 3 three; stk16 x prng x depth

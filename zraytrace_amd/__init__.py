@@ -428,3 +428,13 @@ def write_ppm(path: str, image) -> None:
     img = np.ascontiguousarray(image, dtype=np.float32)
     h, w, _ = img.shape
     check(lib().zrt_image_write_ppm(os.fsencode(path), img.ctypes.data_as(C.POINTER(C.c_float)), w, h))
+
+
+def debug_lds_plans(scene) -> int:
+    """Host-side check of every LDS layout the launch code can plan for this scene
+    (zrt_debug_lds_plans; no device): returns the number of plans checked, raises
+    ZrtError naming the first overlapping / misaligned / oversized region."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    n = C.c_uint32()
+    check(lib().zrt_debug_lds_plans(view, C.byref(n)))
+    return n.value

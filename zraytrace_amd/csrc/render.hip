@@ -1111,42 +1111,23 @@ struct WideNode {
   float4 nx, ny, nz, fx, fy, fz, ra;
 };
 
-// The top wide nodes in LDS are read through an LDS-typed (32-bit) pointer of
-// native 4-vectors (one ds_read_b128 each): a traversal's current node is kept
-// as an index and addressed per use, never as a 64-bit generic pointer that
-// would select between LDS and global memory at every read (and cost a VGPR
-// pair across the whole loop).
-typedef float nf4 __attribute__((ext_vector_type(4)));
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(3))) nf4 lds_cnf4;
-#else
-typedef const nf4 lds_cnf4;
-#endif
-__device__ __forceinline__ float4 f4(nf4 v) { return make_float4(v.x, v.y, v.z, v.w); }
-
-__device__ __forceinline__ void wide_set(float4 m0, float4 m1, float4 m2, float4 m3, float4 m4, float4 m5, float4 m6,
-                                         bool sx, bool sy, bool sz, WideNode& w) {
+__device__ __forceinline__ void wide_load(const float4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
 #if ZRT_OCT_COPIES
   (void)sx; (void)sy; (void)sz;
-  w.nx = m0; w.ny = m1; w.nz = m2; w.fx = m3; w.fy = m4; w.fz = m5;
+  w.nx = q[0]; w.ny = q[1]; w.nz = q[2]; w.fx = q[3]; w.fy = q[4]; w.fz = q[5]; w.ra = q[6];
 #else
+  const float4 m0 = q[0], m1 = q[1], m2 = q[2], m3 = q[3], m4 = q[4], m5 = q[5];
   w.nx = sx ? m3 : m0; w.fx = sx ? m0 : m3;
   w.ny = sy ? m4 : m1; w.fy = sy ? m1 : m4;
   w.nz = sz ? m5 : m2; w.fz = sz ? m2 : m5;
+  w.ra = q[6];
 #endif
-  w.ra = m6;
-}
-__device__ __forceinline__ void wide_load(const float4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
-  wide_set(q[0], q[1], q[2], q[3], q[4], q[5], q[6], sx, sy, sz, w);
-}
-__device__ __forceinline__ void wide_load(lds_cnf4* __restrict__ q, bool sx, bool sy, bool sz, WideNode& w) {
-  wide_set(f4(q[0]), f4(q[1]), f4(q[2]), f4(q[3]), f4(q[4]), f4(q[5]), f4(q[6]), sx, sy, sz, w);
 }
 
 // Where a ray reads the wide tree: its octant's copy (global memory) and that
 // copy's top levels in LDS.
 struct WideView {
-  lds_cnf4* __restrict__ top;      // this octant's copy of the top nodes in LDS
+  const float4* __restrict__ top;  // this octant's copy of the top nodes in LDS
   uint32_t base;                   // float4 offset of this octant's copy (< 2^32)
   uint32_t n_top;
   bool sx, sy, sz;
@@ -1164,24 +1145,15 @@ __device__ __forceinline__ WideView wide_view(const KArgs& a, const RayT& r, con
   const uint32_t oct = 0;
   v.base = 0;
 #endif
-  v.top = (lds_cnf4*)(lds_top) + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
+  v.top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
   v.n_top = ZRT_LDS_TOP ? a.n_top : 0u;
   return v;
 }
 
 // The address of wide node `i` for this ray: LDS for a top-level node, else
-// its octant copy in global memory (a generic pointer: the rare per-axis tests)
+// its octant copy in global memory.
 __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const WideView& v, uint32_t i) {
-  return i < v.n_top ? (const float4*)(v.top + 8u * i) : a.wnodes + (v.base + 8u * i);
-}
-// wide node i into w: LDS for a top-level node, else global memory
-__device__ __forceinline__ void wide_load_at(const KArgs& a, const WideView& v, uint32_t i, WideNode& w) {
-  if (i < v.n_top) wide_load(v.top + 8u * i, v.sx, v.sy, v.sz, w);
-  else wide_load(a.wnodes + (v.base + 8u * i), v.sx, v.sy, v.sz, w);
-}
-// float4 j of wide node i
-__device__ __forceinline__ float4 wide_f4(const KArgs& a, const WideView& v, uint32_t i, uint32_t j) {
-  return i < v.n_top ? f4(v.top[8u * i + j]) : a.wnodes[v.base + 8u * i + j];
+  return i < v.n_top ? v.top + 8u * i : a.wnodes + (v.base + 8u * i);
 }
 
 // FAST: near-first over the 4-wide tree (accel_build.cpp), stored once per
@@ -1199,12 +1171,12 @@ __device__ __forceinline__ float4 wide_f4(const KArgs& a, const WideView& v, uin
 // (pushing the farther inner children), intersects the opened leaves and loads
 // the next node into `w` / q.  Returns false when the traversal is over (then
 // the order-hazard test of wide_finish follows).  Its state between calls is
-// (w, qn, sp, best_t, best) and the lane's stack column, so a traversal can be
+// (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
 template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK, bool GUARD = true>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
-                                          uint32_t& qn, uint32_t& sp, float& best_t, int& best,
+                                          const float4*& q, uint32_t& sp, float& best_t, int& best,
                                           uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
                                           Coh& coh) {
   const int stride = kBlock;
@@ -1316,7 +1288,6 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   const bool w0 = o0 && (pg || !ZRT_SURE(s0)), w1 = o1 && (pg || !ZRT_SURE(s1));
   const bool w2 = o2 && (pg || !ZRT_SURE(s2)), w3 = o3 && (pg || !ZRT_SURE(s3));
   if (w0 || w1 || w2 || w3) {  // rare: an interval within the margin, decide per axis
-    const float4* q = wide_node_ptr(a, v, qn);
     if (w0) o0 = loose_slot(q, 0, r, tb, sx, sy, sz, s0.en, gg);
     if (w1) o1 = loose_slot(q, 1, r, tb, sx, sy, sz, s1.en, gg);
     if (w2) o2 = loose_slot(q, 2, r, tb, sx, sy, sz, s2.en, gg);
@@ -1343,7 +1314,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if (r##K < -kSphereSlotBias) {                                                                             \
     o##K = !pw && !deg && ZRT_SURE(s##K);                                                                    \
     if (!o##K && !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, Eg) > 0.001f)          \
-      o##K = static_ok_slot(wide_node_ptr(a, v, qn), K, r, sx, sy, sz, s##K.en);                             \
+      o##K = static_ok_slot(q, K, r, sx, sy, sz, s##K.en);                                                   \
     r##K += kSphereSlotBias;                                                                                 \
   }
     ZRT_SPHERE_SLOT(0)
@@ -1355,7 +1326,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
 #endif
 #undef ZRT_SURE
   const int l0 = o0 ? r0 : 0, l1 = o1 ? r1 : 0, l2 = o2 ? r2 : 0, l3 = o3 ? r3 : 0;
-  const uint32_t leaf_n = qn;  // (the leaves are intersected after the next node is chosen)
+  const float4* leaf_q = q;  // (the leaves are intersected after the next node is chosen)
   int32_t next = -1;
   // inner slots that pass, keyed by entry distance
   float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
@@ -1421,7 +1392,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
     uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
     if (open != 0) {
-      const float4 rb = wide_f4(a, v, leaf_n, 7);
+      const float4 rb = leaf_q[7];
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(open);
         open &= open - 1u;
@@ -1448,7 +1419,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
       } while (open != 0);
     }
   } else if ((l0 | l1 | l2 | l3) != 0) {
-    const float4 rb = wide_f4(a, v, leaf_n, 7);  // (loaded with the node instead: 3.6 % slower, 2 spills)
+    const float4 rb = leaf_q[7];  // (loaded with the node instead: 3.6 % slower, 2 spills)
 #define ZRT_WIDE_LEAF(L, RB, K)                                                                     \
   if (L != 0) {                                                                                     \
     const int pb = as_int(RB);                                                                      \
@@ -1469,12 +1440,14 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     coh.unodes += uni ? 1u : 0u;
   }
   if (next < 0) return false;
-  qn = (uint32_t)next;
   if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS (ds_read)
-    wide_load(v.top + 8u * (uint32_t)next, sx, sy, sz, w);
+    const float4* __restrict__ t = v.top + 8u * (uint32_t)next;
+    q = t;
+    wide_load(t, sx, sy, sz, w);
   } else {
     const uint32_t at = v.base + 8u * (uint32_t)next;  // this ray's octant copy
     const float4* __restrict__ g = a.wnodes + at;
+    q = g;
     const uint32_t fa = __builtin_amdgcn_readfirstlane(at);
     if (SCALAR_NODES && __ballot(at != fa) == 0ull) {  // one node in every active lane: scalar loads
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1528,10 +1501,10 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const WideView v = wide_view(a, r, lds_top);
   uint32_t sp = 0;
   // the root is node 0 of this octant's copy (in LDS when the top levels are)
-  uint32_t qn = 0;
+  const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
   WideNode w;
-  wide_load_at(a, v, 0u, w);
-  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves,
+  wide_load(q, v.sx, v.sy, v.sz, w);
+  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves,
                                                            c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
@@ -1681,24 +1654,6 @@ __device__ __forceinline__ void flush_scanline(unsigned long long* __restrict__ 
     if (d) atomicAdd(&rows[3 * py + 0], (unsigned long long)d);
     if (r) atomicAdd(&rows[3 * py + 1], (unsigned long long)r);
     if (b) atomicAdd(&rows[3 * py + 2], (unsigned long long)b);
-  }
-}
-
-// ZRT_FLAG_SCANLINES for a wave whose events are ballot masks (lane p = pixel p of
-// the 8x8 tile whose bottom row is y0): each tile row's count added to its frame
-// row by lane 0.  Called with the whole wave converged.
-__device__ __forceinline__ void scanline_masks(unsigned long long* __restrict__ rows, uint32_t y0, uint32_t height,
-                                               uint64_t md, uint64_t mr, uint64_t mb) {
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t py = y0 + k;
-    const uint32_t d = __popcll((md >> (8 * k)) & 0xffull), r = __popcll((mr >> (8 * k)) & 0xffull);
-    const uint32_t b = __popcll((mb >> (8 * k)) & 0xffull);
-    if (py < height && (d | r | b) && __lane_id() == 0) {
-      if (d) atomicAdd(&rows[3 * py + 0], (unsigned long long)d);
-      if (r) atomicAdd(&rows[3 * py + 1], (unsigned long long)r);
-      if (b) atomicAdd(&rows[3 * py + 2], (unsigned long long)b);
-    }
   }
 }
 
@@ -1973,11 +1928,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   uint32_t depth_left = 0;  // attenuations stacked so far: max_depth - depth_left
   Rng<PRNG> rng;
   rng.init(0);
-  // raytrace.zig:20-34's Progress counters of the current unit, wave-uniform (SGPRs):
-  // each step's events are ballots taken where the wave is converged, so no lane
-  // carries a counter across the traversal (three fewer long-lived VGPRs)
-  uint32_t s_depth = 0, s_refl = 0, s_bg = 0;
-  uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
+  uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
   ExcessAcc excess;  // REFERENCE traversal, STATS flavour only
@@ -2008,12 +1959,10 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
         if (cur_lt != 0xffffffffu)  // the finished unit's chunk sums, [chunk][pixel slot]: one 1 KiB store per wave
           a.partial[chunk_j * a.n_slots + cur_lt * 64u + (uint32_t)lane] = make_float4(acc_r, acc_g, acc_b, 0.0f);
         if (a.unit_cost && cur_lt != 0xffffffffu && lane == 0) a.unit_cost[cur_lt] = iters;
-        if ((s_depth | s_refl | s_bg) != 0u && lane == 0) {  // the finished unit's Progress counters
-          if (s_depth) atomicAdd(&a.counters[kDepthHits], (unsigned long long)s_depth);
-          if (s_refl) atomicAdd(&a.counters[kReflections], (unsigned long long)s_refl);
-          if (s_bg) atomicAdd(&a.counters[kBackground], (unsigned long long)s_bg);
+        if (a.scanlines && cur_lt != 0xffffffffu) {  // the finished unit's counters, per frame row
+          flush_scanline(a.scanlines, y0 + ((uint32_t)lane >> 3), a.height, lane, c_depth, c_refl, c_bg);
+          c_depth = c_refl = c_bg = 0;  // (so the launch totals are the rows' sums)
         }
-        s_depth = s_refl = s_bg = 0;
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.work_counter, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
@@ -2042,8 +1991,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       c_loops += lane == 0 ? 1u : 0u;
       c_lsteps += runnable ? 1u : 0u;
     }
-    uint32_t e_depth = 0, e_refl = 0, e_bg = 0;  // this step's events in this lane
-    if (runnable) {
+    if (!runnable) continue;
+
     // ---- a new sample: jitter + Camera.getRay (raytrace.zig:173-175)
     if (!in_sample) {
       const uint32_t px = x0 + ((uint32_t)lane & 7u), py = y0 + ((uint32_t)lane >> 3);
@@ -2065,7 +2014,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     bool path_end = false, sky = false;
     V3 L = mk(0.0f, 0.0f, 0.0f);
     if (depth_left == 0) {
-      ++e_depth;
+      ++c_depth;
       path_end = true;
     } else {
       if (STATS) ++c_rays;
@@ -2108,7 +2057,7 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       }
       if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[2] += t - t0; t0 = t; }
       shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
-                        sky, L, e_bg, e_refl, c_shade, c_tex, coh);
+                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
     }
 
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[3] += t - t0; t0 = t; }
@@ -2123,14 +2072,6 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
       if (++sample == unit_end) active = false;  // chunk done: its sequential sum, stored when the unit ends
     }
     if (ZRT_PROFILE) { const uint64_t t = prof_stamp(); pf[4] += t - t0; }
-    }  // runnable
-    {  // the wave is converged again: its step's events as ballots
-      const uint64_t md = __ballot(e_depth != 0u), mr = __ballot(e_refl != 0u), mb = __ballot(e_bg != 0u);
-      s_depth += (uint32_t)__popcll(md);
-      s_refl += (uint32_t)__popcll(mr);
-      s_bg += (uint32_t)__popcll(mb);
-      if (a.scanlines) scanline_masks(a.scanlines, y0, a.height, md, mr, mb);
-    }
   }
   if (ZRT_PROFILE && lane == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(&a.counters[kProfSlot + k], (unsigned long long)pf[k]);
@@ -2141,7 +2082,9 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
     }
   }
 
-  // (the loop leaves when the counter is exhausted, after flushing its last unit)
+  wave_add_u64(&a.counters[kDepthHits], c_depth);
+  wave_add_u64(&a.counters[kReflections], c_refl);
+  wave_add_u64(&a.counters[kBackground], c_bg);
   if (STATS) {
     wave_add_u64(&a.counters[kRays], c_rays);
     wave_add_u64(&a.counters[kNodes], c_nodes);
@@ -2229,7 +2172,7 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
-  uint32_t qn = 0;  // the lane's current node (LDS or global)
+  const float4* q = nullptr;  // the lane's current node (LDS or global)
   uint32_t c_rays = 0, c_refl = 0, c_bg = 0, c_depth = 0, c_nodes = 0, c_tri = 0, c_sph = 0;
   uint32_t c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
@@ -2244,12 +2187,12 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
       WideNode w;
       if (trav) {
         v = wide_view(a, r, lds_top);
-        wide_load_at(a, v, qn, w);  // the suspended node (re)loaded
+        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
       }
       for (;;) {
         if (trav) {
           // (its lanes' nodes are rarely one: no scalar-load test, C5 -1.4 % with it)
-          if (!wide_iter<STATS, StackT, false, true, false>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, false, true, false>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             trav = false;
@@ -2338,7 +2281,10 @@ __device__ __forceinline__ void render_loop_wf(const KArgs& a) {
         best_t = __builtin_inff();
     best = -1;
     sp = 0;
-    qn = 0;  // the root of the ray's octant copy
+    {
+      const WideView v = wide_view(a, r, lds_top);
+      q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+    }
     trav = true;
   }
 
@@ -2478,7 +2424,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   float best_t = __builtin_inff();
   int best = -1;
   uint32_t sp = 0;
-  uint32_t qn = 0;  // the lane's current node
+  const float4* q = nullptr;
   uint32_t c_rays = 0, c_nodes = 0, c_tri = 0, c_sph = 0, c_shade = 0, c_tex = 0, c_leaves = 0, c_replays = 0;
   Coh coh;  // STATS
   uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0;
@@ -2492,7 +2438,7 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
       WideNode w;
       if (trav) {
         v = wide_view(a, r, lds_top);
-        wide_load_at(a, v, qn, w);  // the suspended node (re)loaded
+        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
       }
       for (;;) {
         const uint64_t idle = __ballot(!trav);
@@ -2513,15 +2459,15 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
             best = -1;
             sp = 0;
             v = wide_view(a, r, lds_top);
-            qn = 0;  // the root of the ray's octant copy
-            wide_load_at(a, v, 0u, w);
+            q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+            wide_load(q, v.sx, v.sy, v.sz, w);
             trav = true;
           }
           const uint32_t n_idle = (uint32_t)__builtin_popcountll(idle);
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, qn, sp, best_t, best, c_nodes, c_leaves, c_tri,
+          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
                                                c_sph, coh)) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
@@ -4998,6 +4944,38 @@ int zrt_debug_math(int fn, const float* x, const float* y, float* out, uint32_t 
     HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, dout.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
+  if (!n_checked) return fail(ZRT_E_INVALID, "null argument");
+  *n_checked = 0;
+  int rc = zrt::validate_scene(scene);
+  if (rc) return rc;
+  try {
+    zrt::HostScene h;
+    zrt::flatten_scene(&h, scene, scene->n_prims > 10, -1);  // (the host BVH build: no device)
+    const uint32_t n_mats = uint32_t(h.mats.size());
+    const uint32_t ref_depth = h.use_bvh ? h.bvh_depth + 2 : 0;
+    std::string where;
+    for (int mode : {0, 1, 2, 3}) {
+      for (int loop = 0; loop < (mode == 3 ? 3 : 1); ++loop) {  // lockstep, wavefront, path pool
+        for (bool stk16 : {true, false}) {
+          for (uint32_t prng : {uint32_t(ZRT_PRNG_XOROSHIRO128), uint32_t(ZRT_PRNG_XOSHIRO256)}) {
+            for (uint32_t depth : {0u, 1u, 2u, 5u, 20u, 50u}) {
+              const uint32_t sd = mode == 3 ? std::max(h.wide_stack, ref_depth) : ref_depth;
+              where = "mode " + std::to_string(mode) + " loop " + std::to_string(loop) + " stk16 " +
+                      std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " + std::to_string(depth);
+              (void)zrt::plan_lds(h.n_top, n_mats, mode, stk16, sd, depth, loop == 1, loop == 2, prng);
+              ++*n_checked;
+            }
+          }
+        }
+      }
+    }
+    (void)where;
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
