@@ -324,4 +324,5 @@ def test_lds_plans_disjoint(scenes, index):
     rows, materials) disjoint, inside the plan and float4-aligned, and the lockstep
     plan inside its 6-block share (render.hip check_plan).  No device needed."""
     n = z.debug_lds_plans(scenes(index))
-    assert n == 4 * 0 + (1 + 1 + 1 + 3) * 2 * 2 * 6  # modes 0-2 one loop each, mode 3 three; stk16 x prng x depth
+    # modes 0-2 one loop each, mode 3 lockstep / wavefront / pool (full and compressed nodes); x stk16 x prng x depth
+    assert n == (1 + 1 + 1 + 1 + 1 + 2) * 2 * 2 * 6

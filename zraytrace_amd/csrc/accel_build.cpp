@@ -333,3 +333,123 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
 }
 
 }  // namespace zrt
+
+namespace zrt {
+
+namespace {
+// One axis of a node: the step exponent and origin multiple with every plane of
+// [lo, hi] an exact f32 origin + q * step, q in 0..255.  False if none exists.
+bool quant_axis(double lo, double hi, int* e_out, double* m0_out) {
+  if (!(std::isfinite(lo) && std::isfinite(hi) && lo <= hi)) return false;
+  int e = -126;  // the smallest normal step
+  if (hi > lo) e = std::max(e, int(std::floor(std::log2((hi - lo) / 255.0))) - 1);
+  for (; e <= 127; ++e) {
+    const double s = std::ldexp(1.0, e);
+    const double m0 = std::floor(lo / s), m1 = std::ceil(hi / s);
+    if (m1 - m0 <= 255.0 && std::fabs(m0) + 256.0 < 16777216.0) {
+      *e_out = e;
+      *m0_out = m0;
+      return true;
+    }
+  }
+  return false;
+}
+}  // namespace
+
+QuantWide quantize_wide(const WideBvh& w) {
+  QuantWide out;
+  const uint32_t n = w.n_nodes;
+  out.n_nodes = n;
+  std::vector<float4v> base(size_t(n) * kQuantNodeF4);  // unswapped; bytes as min (near) / max (far)
+  struct Planes {
+    uint32_t qmin[3], qmax[3];  // bytes of slots 0..3, per axis
+  };
+  std::vector<Planes> planes(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const float4v* q = &w.nodes[8 * size_t(i)];
+    int32_t ref[4], ref_b[4];
+    std::memcpy(ref, q[6].v, 16);
+    std::memcpy(ref_b, q[7].v, 16);
+    bool empty[4];
+    for (int k = 0; k < 4; ++k) empty[k] = q[0].v[k] > q[3].v[k];  // (min = +inf, max = -inf)
+    uint32_t word[16] = {0};
+    Planes& P = planes[i];
+    for (int a = 0; a < 3; ++a) {
+      double lo = INFINITY, hi = -INFINITY;
+      for (int k = 0; k < 4; ++k)
+        if (!empty[k]) {
+          lo = std::min(lo, double(q[a].v[k]));
+          hi = std::max(hi, double(q[3 + a].v[k]));
+        }
+      int e = 0;
+      double m0 = 0.0;
+      if (lo > hi) {  // no child
+        lo = hi = 0.0;
+      }
+      if (!quant_axis(lo, hi, &e, &m0)) return out;  // (ok stays false)
+      const double s = std::ldexp(1.0, e);
+      const float origin = float(m0 * s);
+      if (double(origin) != m0 * s) return out;
+      std::memcpy(&word[a], &origin, 4);
+      word[3] |= uint32_t(e + 127) << (8 * a);
+      P.qmin[a] = P.qmax[a] = 0;
+      for (int k = 0; k < 4; ++k) {
+        uint32_t qn = 255, qf = 0;  // an empty slot: near above far (never opened: its ref is kEmptyRef)
+        if (!empty[k]) {
+          const double mn = q[a].v[k], mx = q[3 + a].v[k];
+          qn = uint32_t(std::floor(mn / s) - m0);
+          qf = uint32_t(std::ceil(mx / s) - m0);
+          // decoded exactly, outward (the child's box within the quantized one)
+          const float dn = float(double(origin) + double(qn) * s), df = float(double(origin) + double(qf) * s);
+          if (qn > 255 || qf > 255 || !(double(dn) <= mn) || !(double(df) >= mx) ||
+              double(dn) != double(origin) + double(qn) * s || double(df) != double(origin) + double(qf) * s)
+            return out;
+        }
+        P.qmin[a] |= qn << (8 * k);
+        P.qmax[a] |= qf << (8 * k);
+      }
+    }
+    for (int k = 0; k < 4; ++k) {
+      int32_t r = ref[k];
+      if (empty[k]) {
+        r = kEmptyRef;
+      } else if (r < 0) {  // a leaf: its record
+        const uint32_t L = out.n_leaves++;
+        const bool sphere = r < -kSphereSlotBias;
+        const int32_t a = sphere ? r + kSphereSlotBias : r;
+        float4v rec[2];
+        for (int j = 0; j < 3; ++j) {
+          rec[0].v[j] = q[j].v[k];
+          rec[1].v[j] = q[3 + j].v[k];
+        }
+        std::memcpy(&rec[0].v[3], &a, 4);
+        std::memcpy(&rec[1].v[3], &ref_b[k], 4);
+        out.leaves.push_back(rec[0]);
+        out.leaves.push_back(rec[1]);
+        r = -int32_t(L) - 1 - (sphere ? kSphereSlotBias : 0);
+      }
+      std::memcpy(&word[10 + k], &r, 4);
+    }
+    std::memcpy(&base[size_t(i) * kQuantNodeF4], word, sizeof(word));
+  }
+  // the octant copies: axis k's near / far bytes swapped where the direction is negative
+  out.nodes.resize(8 * size_t(n) * kQuantNodeF4);
+  for (uint32_t o = 0; o < 8; ++o) {
+    float4v* dst = out.nodes.data() + size_t(o) * n * kQuantNodeF4;
+    std::memcpy(dst, base.data(), base.size() * sizeof(float4v));
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t word[16];
+      std::memcpy(word, &dst[size_t(i) * kQuantNodeF4], sizeof(word));
+      for (int a = 0; a < 3; ++a) {
+        const bool neg = (o >> a) & 1u;
+        word[4 + a] = neg ? planes[i].qmax[a] : planes[i].qmin[a];
+        word[7 + a] = neg ? planes[i].qmin[a] : planes[i].qmax[a];
+      }
+      std::memcpy(&dst[size_t(i) * kQuantNodeF4], word, sizeof(word));
+    }
+  }
+  out.ok = true;
+  return out;
+}
+
+}  // namespace zrt

@@ -53,3 +53,39 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels =
 inline bool ref_is_sphere(int32_t ref) { return ref < 0 && ((-(int64_t(ref) + 1)) & 1) == 0; }
 
 }  // namespace zrt
+
+namespace zrt {
+
+// Compressed wide nodes for trees past the caches (render.hip wide_iter_q,
+// DESIGN.md §3 "Compressed nodes"): 64 B per node instead of 128 B.
+//   node = 4 x float4 (16 words), per ray-octant copy:
+//     w0-2  origin.xyz (f32), w3 the per-axis step exponents, biased by 127
+//           (step_k = 2^(e_k - 127), a normal float; bits 0-7 x, 8-15 y, 16-23 z)
+//     w4-6  near planes x, y, z of slots 0..3 as bytes (byte k = slot k)
+//     w7-9  far planes x, y, z (bytes); near / far pre-swapped per octant as
+//           the full nodes' planes are
+//     w10-13 refs of slots 0..3: inner child = node index (>= 0); leaf =
+//           -(leaf record + 1), minus kSphereSlotBias for a sphere leaf;
+//           empty slot = kEmptyRef
+//     w14-15 0
+//   A plane is origin + q * step, computed exactly in f32 (origin is a multiple
+//   of step and |origin / step| + 255 < 2^24), and quantized outward: every
+//   child box contains the full node's box of that slot, so the culls stay
+//   supersets (any containing box is allowed, accel_build.cpp's header).
+//   leaf record = 2 x float4: {min.xyz, prim ref a}, {max.xyz, prim ref b}: the
+//   reference leaf's own box bit for bit (the loose test and the hazard entry
+//   read it) and its one or two primitive-slot refs.
+constexpr int32_t kEmptyRef = INT32_MIN;
+constexpr uint32_t kQuantNodeF4 = 4, kLeafRecF4 = 2;
+
+struct QuantWide {
+  std::vector<float4v> nodes;   // 8 octant copies, copy-major: copy o at o * n_nodes * 4
+  std::vector<float4v> leaves;  // kLeafRecF4 per leaf record
+  uint32_t n_nodes = 0, n_leaves = 0;
+  bool ok = false;  // false: a box could not be quantized (a non-finite plane): use the full nodes
+};
+
+// The 8 octant copies of `w`'s nodes (full format, unswapped planes) compressed.
+QuantWide quantize_wide(const WideBvh& w);
+
+}  // namespace zrt

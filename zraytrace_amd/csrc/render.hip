@@ -35,6 +35,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "accel_build.hpp"
@@ -66,7 +67,8 @@ struct KArgs {
   const float4* __restrict__ nodes;
   const float4* __restrict__ prims;
   const float4* __restrict__ shade;
-  const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (8 float4 each)
+  const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (node_f4 float4 each: 8 full, 4 compressed)
+  const float4* __restrict__ qleaves;  // compressed nodes' leaf records (kLeafRecF4 float4 each), else null
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;    // f32 RGB images
   const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
@@ -92,6 +94,7 @@ struct KArgs {
   uint32_t chunk, n_chunks, sync;  // a work unit = one chunk of one tile
   uint32_t n_slots;  // this launch's pixel slots (tiles x 64): the stride of a chunk in partial
   uint32_t wide_stride;  // float4s per octant copy of the wide tree
+  uint32_t node_f4;      // float4s per wide node: 8 (full, wide_iter) or 4 (compressed, wide_iter_q)
   uint32_t lds_rows;     // FAST: stack rows in LDS; rows lds_rows.. stack_depth-1 in stack_ovf
   uint32_t ref_stack;    // rows the reference traversal needs (FAST's order-hazard replay)
   const uint32_t* __restrict__ leaf_of_slot;  // primitive slot -> its reference BVH leaf node
@@ -998,20 +1001,13 @@ __device__ __forceinline__ bool static_ok(float nx, float ny, float nz, float fx
 // gg: the grazing-triangle guard's spatial widening of this ray (0: off), added to
 // the leaf's own slack in both tests; the entry stays the exact loose entry, so a
 // best hit found below it (a leaf opened only by the widening) is replayed.
-__device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, const RayT& r, float tb,
-                                           bool sx, bool sy, bool sz, float& entry, float gg = 0.0f) {
+// (planes: the slot's near / far planes in the ray's octant, bx / by / bz near, cx / cy / cz far)
+__device__ __forceinline__ bool loose_planes(float bx, float by, float bz, float cx, float cy, float cz, const RayT& r,
+                                             float tb, float& entry, float gg = 0.0f) {
   const float t_min = 0.001f;
-  const float* f = reinterpret_cast<const float*>(q) + k;
-#if ZRT_OCT_COPIES
-  (void)sx; (void)sy; (void)sz;
-  const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
-#else
-  const int px = sx ? 12 : 0, py = sy ? 16 : 4, pz = sz ? 20 : 8;
-  const int qx = sx ? 0 : 12, qy = sy ? 4 : 16, qz = sz ? 8 : 20;
-#endif
-  const float nx = (f[px] - r.ox) * r.ix, fx = (f[qx] - r.ox) * r.ix;
-  const float ny = (f[py] - r.oy) * r.iy, fy = (f[qy] - r.oy) * r.iy;
-  const float nz = (f[pz] - r.oz) * r.iz, fz = (f[qz] - r.oz) * r.iz;
+  const float nx = (bx - r.ox) * r.ix, fx = (cx - r.ox) * r.ix;
+  const float ny = (by - r.oy) * r.iy, fy = (cy - r.oy) * r.iy;
+  const float nz = (bz - r.oz) * r.iz, fz = (cz - r.oz) * r.iz;
   // the exact loose entry (the order-hazard test's E; wide_iter's en when its slabs are not widened)
   entry = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, t_min));
   if (!ZRT_GRAZE_SLACK)
@@ -1021,9 +1017,9 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   // the leaf's own coordinate slack (ray_slack): g = 2 x 2^-19 x its largest |coordinate|,
   // g |1/d_k| on axis k; a hit below the leaf's entry by that still counts against tb
   const float cl = __builtin_fmaxf(
-      __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(f[px]), __builtin_fabsf(f[qx])),
-                      __builtin_fmaxf(__builtin_fabsf(f[py]), __builtin_fabsf(f[qy]))),
-      __builtin_fmaxf(__builtin_fabsf(f[pz]), __builtin_fabsf(f[qz])));
+      __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(cx)),
+                      __builtin_fmaxf(__builtin_fabsf(by), __builtin_fabsf(cy))),
+      __builtin_fmaxf(__builtin_fabsf(bz), __builtin_fabsf(cz)));
   const float g = __builtin_fmaf(cl, r.gm, gg);
   const float gx = paxis_t(g, r.ix), gy = paxis_t(g, r.iy), gz = paxis_t(g, r.iz);
   const float tl = tb + __builtin_fmaxf(__builtin_fmaxf(gx, gy), gz);
@@ -1034,6 +1030,18 @@ __device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, 
   const float en = __builtin_fmaxf(__builtin_fmaxf(nx - gx, ny - gy), __builtin_fmaxf(nz - gz, t_min));
   const float ex = __builtin_fminf(__builtin_fminf(fx + gx, fy + gy), __builtin_fminf(fz + gz, tl));
   return loose && !(en > ex * (ZRT_GRAZE_LEAF ? 1.0000153f + r.gl * ray_m(r) : ray_rel(r, ray_m(r))));
+}
+__device__ __forceinline__ bool loose_slot(const float4* __restrict__ q, int k, const RayT& r, float tb,
+                                           bool sx, bool sy, bool sz, float& entry, float gg = 0.0f) {
+  const float* f = reinterpret_cast<const float*>(q) + k;
+#if ZRT_OCT_COPIES
+  (void)sx; (void)sy; (void)sz;
+  const int px = 0, py = 4, pz = 8, qx = 12, qy = 16, qz = 20;
+#else
+  const int px = sx ? 12 : 0, py = sy ? 16 : 4, pz = sz ? 20 : 8;
+  const int qx = sx ? 0 : 12, qy = sy ? 4 : 16, qz = sz ? 8 : 20;
+#endif
+  return loose_planes(f[px], f[py], f[pz], f[qx], f[qy], f[qz], r, tb, entry, gg);
 }
 
 // static_ok of leaf slot k, its slab distances recomputed from the node in memory
@@ -1072,7 +1080,7 @@ constexpr uint32_t kOctCopies = ZRT_OCT_COPIES ? 8u : 1u;
 // vector-memory data return (TD) is what the FAST loop saturates:
 // these node reads come from LDS instead.  All threads of the block call this.
 __device__ __forceinline__ void fill_lds_top(const KArgs& a, float4* __restrict__ top) {
-  const uint32_t per = a.n_top * 8u;  // float4 per octant copy
+  const uint32_t per = a.n_top * a.node_f4;  // float4 per octant copy
   for (uint32_t i = threadIdx.x; i < per * kOctCopies; i += kBlock) {
     const uint32_t o = i / per, j = i - o * per;
     top[i] = a.wnodes[o * a.wide_stride + j];
@@ -1145,7 +1153,7 @@ __device__ __forceinline__ WideView wide_view(const KArgs& a, const RayT& r, con
   const uint32_t oct = 0;
   v.base = 0;
 #endif
-  v.top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * 8u);
+  v.top = lds_top + (ZRT_OCT_COPIES ? oct : 0u) * (a.n_top * a.node_f4);
   v.n_top = ZRT_LDS_TOP ? a.n_top : 0u;
   return v;
 }
@@ -1491,6 +1499,266 @@ __device__ __forceinline__ void wide_finish(const KArgs& a, const RayT& r, Stack
 #endif
     reference_replay<StackT>(a, r, stk, gl, best_t, best, !far);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Compressed wide nodes (accel_build.hpp quantize_wide; DESIGN.md §3
+// "Compressed nodes"): 64 B per node - the origin and per-axis power-of-two
+// step, the 24 planes as bytes, the refs - instead of 128 B, for trees past the
+// caches (the C5 mesh: 475 MB of octant copies become 238 MB).  A plane decodes
+// exactly (origin + q * step is an f32 by construction), so the slab distances
+// and every margin are wide_iter's; the quantized boxes contain the full nodes'
+// boxes, so the culls are supersets.  A leaf slot's exact box (the reference's,
+// bit for bit) and its primitive refs come from its leaf record, read when the
+// quantized box passes: every decision wide_iter takes from the leaf's planes -
+// the narrowed and loose tests, a sphere slot's static test, the hazard entry -
+// is taken from the record's planes with wide_iter's formulas.
+struct WideNodeQ {
+  float4 f0, f1, f2, f3;  // {origin.xyz, steps}, {near x/y/z, far x}, {far y/z, ref 0/1}, {ref 2/3, 0, 0}
+};
+template <class P>
+__device__ __forceinline__ void qnode_load(P q, WideNodeQ& w) {
+  w.f0 = q[0];
+  w.f1 = q[1];
+  w.f2 = q[2];
+  w.f3 = q[3];
+}
+// plane byte k of `word`: origin + q * step (exact: a product of a byte and a
+// power of two, then a sum the encoder made representable)
+__device__ __forceinline__ float qplane(uint32_t word, int k, float step, float origin) {
+  return __builtin_fmaf((float)((word >> (8 * k)) & 0xffu), step, origin);
+}
+__device__ __forceinline__ float qstep(uint32_t e8) { return __uint_as_float(e8 << 23); }
+
+// static_ok (aabb.zig:109-127 against t_max = +inf) of a box given by its planes in
+// the ray's octant, and its exact loose entry
+__device__ __forceinline__ bool static_ok_planes(float bx, float by, float bz, float cx, float cy, float cz,
+                                                 const RayT& r, float& entry) {
+  const float nx = (bx - r.ox) * r.ix, ny = (by - r.oy) * r.iy, nz = (bz - r.oz) * r.iz;
+  entry = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, 0.001f));
+  return static_ok(nx, ny, nz, (cx - r.ox) * r.ix, (cy - r.oy) * r.iy, (cz - r.oz) * r.iz);
+}
+
+template <bool STATS, class StackT, bool PAXIS = true, bool GUARD = true>
+__device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const WideView& v,
+                                            StackT* __restrict__ stk, uint32_t gl, WideNodeQ& w,
+                                            const float4*& q, uint32_t& sp, float& best_t, int& best,
+                                            uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri, uint32_t& c_sph,
+                                            Coh& coh) {
+  (void)q;
+  const int stride = kBlock;
+  const uint32_t cap = a.stack_depth;
+  const uint32_t rows = sizeof(StackT) == 4 ? a.lds_rows : cap;
+  StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
+  const float inf = __builtin_inff();
+  const bool sx = v.sx, sy = v.sy, sz = v.sz;
+  int r0 = as_int(w.f2.z), r1 = as_int(w.f2.w), r2 = as_int(w.f3.x), r3 = as_int(w.f3.y);
+  const float ox = w.f0.x, oy = w.f0.y, oz = w.f0.z;
+  const uint32_t ee = __float_as_uint(w.f0.w);
+  const float stx = qstep(ee & 0xffu), sty = qstep((ee >> 8) & 0xffu), stz = qstep((ee >> 16) & 0xffu);
+  const uint32_t bnx = __float_as_uint(w.f1.x), bny = __float_as_uint(w.f1.y), bnz = __float_as_uint(w.f1.z);
+  const uint32_t bfx = __float_as_uint(w.f1.w), bfy = __float_as_uint(w.f2.x), bfz = __float_as_uint(w.f2.y);
+  const float tb = __builtin_fabsf(best_t) * kOpen;
+  const float m = ray_m(r), rel = ray_rel(r, m), slk = ray_slack(r, a.scene_extent, m);
+  const float px = r.ox * r.ix, py = r.oy * r.iy, pz = r.oz * r.iz;
+  const float pm = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(px), __builtin_fabsf(py)), __builtin_fabsf(pz));
+  const bool deg = !(m < 0x1p100f) || !(pm < 0x1p120f);  // ray_degenerate: nothing opens, wide_finish replays
+  float E2 = pm * kFmaE2;
+  float Eg = E2, gg = 0.0f;
+  // the slab offsets of the near / far planes (wide_iter: p -+ the guard's w)
+  float onx = px, ony = py, onz = pz, ofx = px, ofy = py, ofz = pz;
+  if (ZRT_GUARD && GUARD && PAXIS && __builtin_expect(r.gk > 0.0f, 0)) {  // scene-uniform: a scalar branch
+    const float g = guard_grow(a, r);
+    gg = g;
+    const float wx = paxis_t(g, r.ix), wy = paxis_t(g, r.iy), wz = paxis_t(g, r.iz);
+    const float wm = __builtin_fmaxf(__builtin_fmaxf(wx, wy), wz);
+    E2 = (pm + wm) * kFmaE2;
+    Eg = __builtin_fmaf(wm, 2.0f, E2);
+    onx = px + wx; ony = py + wy; onz = pz + wz;
+    ofx = px - wx; ofy = py - wy; ofz = pz - wz;
+  }
+#define ZRT_QSLAB(BW, K, ST, OR, OFF, INV) __builtin_fmaf(qplane(BW, K, ST, OR), INV, -(OFF))
+  f2 nx01 = {ZRT_QSLAB(bnx, 0, stx, ox, onx, r.ix), ZRT_QSLAB(bnx, 1, stx, ox, onx, r.ix)};
+  f2 nx23 = {ZRT_QSLAB(bnx, 2, stx, ox, onx, r.ix), ZRT_QSLAB(bnx, 3, stx, ox, onx, r.ix)};
+  f2 ny01 = {ZRT_QSLAB(bny, 0, sty, oy, ony, r.iy), ZRT_QSLAB(bny, 1, sty, oy, ony, r.iy)};
+  f2 ny23 = {ZRT_QSLAB(bny, 2, sty, oy, ony, r.iy), ZRT_QSLAB(bny, 3, sty, oy, ony, r.iy)};
+  f2 nz01 = {ZRT_QSLAB(bnz, 0, stz, oz, onz, r.iz), ZRT_QSLAB(bnz, 1, stz, oz, onz, r.iz)};
+  f2 nz23 = {ZRT_QSLAB(bnz, 2, stz, oz, onz, r.iz), ZRT_QSLAB(bnz, 3, stz, oz, onz, r.iz)};
+  f2 fx01 = {ZRT_QSLAB(bfx, 0, stx, ox, ofx, r.ix), ZRT_QSLAB(bfx, 1, stx, ox, ofx, r.ix)};
+  f2 fx23 = {ZRT_QSLAB(bfx, 2, stx, ox, ofx, r.ix), ZRT_QSLAB(bfx, 3, stx, ox, ofx, r.ix)};
+  f2 fy01 = {ZRT_QSLAB(bfy, 0, sty, oy, ofy, r.iy), ZRT_QSLAB(bfy, 1, sty, oy, ofy, r.iy)};
+  f2 fy23 = {ZRT_QSLAB(bfy, 2, sty, oy, ofy, r.iy), ZRT_QSLAB(bfy, 3, sty, oy, ofy, r.iy)};
+  f2 fz01 = {ZRT_QSLAB(bfz, 0, stz, oz, ofz, r.iz), ZRT_QSLAB(bfz, 1, stz, oz, ofz, r.iz)};
+  f2 fz23 = {ZRT_QSLAB(bfz, 2, stz, oz, ofz, r.iz), ZRT_QSLAB(bfz, 3, stz, oz, ofz, r.iz)};
+#undef ZRT_QSLAB
+  // per-axis widening (wide_iter, paxis_grow): the same terms, kept for the leaf records
+  bool pw = false;
+  float gx = 0.0f, gy = 0.0f, gz = 0.0f;
+  if (ZRT_PAXIS && PAXIS && __builtin_expect(__ballot(m > a.paxis_m) != 0ull, 0)) {
+    pw = true;
+    const float g = paxis_grow(a, r);
+    gx = paxis_t(g, r.ix); gy = paxis_t(g, r.iy); gz = paxis_t(g, r.iz);
+    nx01.x -= gx; nx01.y -= gx; nx23.x -= gx; nx23.y -= gx;
+    ny01.x -= gy; ny01.y -= gy; ny23.x -= gy; ny23.y -= gy;
+    nz01.x -= gz; nz01.y -= gz; nz23.x -= gz; nz23.y -= gz;
+    fx01.x += gx; fx01.y += gx; fx23.x += gx; fx23.y += gx;
+    fy01.x += gy; fy01.y += gy; fy23.x += gy; fy23.y += gy;
+    fz01.x += gz; fz01.y += gz; fz23.x += gz; fz23.y += gz;
+  }
+  const SlotT s0 = slot_interval(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tb);
+  const SlotT s1 = slot_interval(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tb);
+  const SlotT s2 = slot_interval(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tb);
+  const SlotT s3 = slot_interval(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tb);
+  const float rl = pw ? 1.0000153f : rel, sl = (pw ? 0.0f : slk) + E2;
+#if ZRT_GRAZE_LEAF
+  const float rll = pw ? 1.0000153f : 1.0000153f + r.gl * m;
+#else
+  const float rll = rl;
+#endif
+  // the quantized boxes' narrowed test (a superset of the full node's, with its margins)
+  const bool h0 = !deg && !(s0.en > __builtin_fmaf(s0.ex, r0 < 0 ? rll : rl, r0 < 0 ? sl : E2));
+  const bool h1 = !deg && !(s1.en > __builtin_fmaf(s1.ex, r1 < 0 ? rll : rl, r1 < 0 ? sl : E2));
+  const bool h2 = !deg && !(s2.en > __builtin_fmaf(s2.ex, r2 < 0 ? rll : rl, r2 < 0 ? sl : E2));
+  const bool h3 = !deg && !(s3.en > __builtin_fmaf(s3.ex, r3 < 0 ? rll : rl, r3 < 0 ? sl : E2));
+  if (STATS) {
+    ++c_nodes;
+    c_leaves += (r0 < 0) + (r1 < 0) + (r2 < 0) + (r3 < 0);
+  }
+  // candidate leaf slots, decided against their records below: a triangle leaf whose
+  // quantized box passes the narrowed test; a sphere leaf (wide_iter: opened by the
+  // static test against t_max = +inf, never culled by the best) whose quantized exit
+  // can lie past t_min (its exact exit is not larger)
+#define ZRT_QCAND(K) \
+  (r##K < 0 && r##K != kEmptyRef && \
+   (r##K < -kSphereSlotBias ? !deg && s##K.ex + __builtin_fmaf(__builtin_fabsf(s##K.ex), 0x1p-19f, Eg) > 0.001f : h##K))
+  uint32_t open = (ZRT_QCAND(0) ? 1u : 0u) | (ZRT_QCAND(1) ? 2u : 0u) | (ZRT_QCAND(2) ? 4u : 0u) |
+                  (ZRT_QCAND(3) ? 8u : 0u);
+#undef ZRT_QCAND
+  const int l0 = r0, l1 = r1, l2 = r2, l3 = r3;
+  int32_t next = -1;
+  float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
+  float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
+  const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
+  if (__ballot(n > 1u) == 0ull) {
+    if (n != 0) {
+      next = k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3;
+    } else if (sp != 0) {
+      --sp;
+      next = sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+    }
+  } else {
+    cswap(k0, r0, k1, r1);
+    cswap(k2, r2, k3, r3);
+    cswap(k0, r0, k2, r2);
+    cswap(k1, r1, k3, r3);
+    cswap(k1, r1, k2, r2);
+    if (n != 0) {
+      const StackT e0 = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1), e1 = (StackT)(n == 4 ? r2 : r1);
+      const StackT e2 = (StackT)r1;
+      if (sp + 3 <= rows) {
+        stk[sp * stride] = e0;
+        stk[(sp + 1) * stride] = e1;
+        stk[(sp + 2) * stride] = e2;
+      } else {
+        const StackT e[3] = {e0, e1, e2};
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+          if (sp + j < rows) {
+            stk[(sp + j) * stride] = e[j];
+          } else {
+            ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+            if (STATS) ++coh.ovfw;
+          }
+        }
+      }
+      const uint32_t nsp = sp + n - 1;
+      if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, kErrOverflow);
+      sp = min(nsp, cap - 3);
+      next = r0;
+    } else if (sp != 0) {
+      --sp;
+      next = sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+    }
+  }
+  // each lane walks its candidate leaves in slot order: the record's exact box
+  // through wide_iter's leaf decisions, then the primitives
+  while (open != 0) {
+    const uint32_t k = (uint32_t)__builtin_ctz(open);
+    open &= open - 1u;
+    const int ref = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
+    const bool sph = ref < -kSphereSlotBias;
+    const uint32_t L = (uint32_t)(-(sph ? ref + kSphereSlotBias : ref) - 1);
+    const float4 mn = a.qleaves[2 * L], mx = a.qleaves[2 * L + 1];
+    const float bx = sx ? mx.x : mn.x, cx = sx ? mn.x : mx.x;
+    const float by = sy ? mx.y : mn.y, cy = sy ? mn.y : mx.y;
+    const float bz = sz ? mx.z : mn.z, cz = sz ? mn.z : mx.z;
+    // wide_iter's distances of this slot: the same planes, offsets and widening
+    SlotT s = slot_interval(__builtin_fmaf(bx, r.ix, -onx) - gx, __builtin_fmaf(by, r.iy, -ony) - gy,
+                            __builtin_fmaf(bz, r.iz, -onz) - gz, __builtin_fmaf(cx, r.ix, -ofx) + gx,
+                            __builtin_fmaf(cy, r.iy, -ofy) + gy, __builtin_fmaf(cz, r.iz, -ofz) + gz, tb);
+#define ZRT_SURE(S) (__builtin_fmaf(S.en, kFmaSure, Eg) < S.ex)
+    // (in wide_iter's order: the narrowed test, the per-axis test within the margin,
+    // then a sphere slot's static test, which decides it)
+    bool o = !deg && !(s.en > __builtin_fmaf(s.ex, rll, sl));
+    if (o && (pw || gg > 0.0f || !ZRT_SURE(s))) o = loose_planes(bx, by, bz, cx, cy, cz, r, tb, s.en, gg);
+    if (sph) {
+      o = !pw && !deg && ZRT_SURE(s);
+      if (!o && !deg && s.ex + __builtin_fmaf(__builtin_fabsf(s.ex), 0x1p-19f, Eg) > 0.001f)
+        o = static_ok_planes(bx, by, bz, cx, cy, cz, r, s.en);
+    }
+#undef ZRT_SURE
+    if (!o) continue;
+    const int La = as_int(mn.w), pb = as_int(mx.w);
+    const float lp = ZRT_HAZARD_ENTRY ? __builtin_fmaf(s.en, kFmaSure, E2) : -1.0f;
+    if (STATS) {
+      const int f = __builtin_amdgcn_readfirstlane(La);
+      coh.ptests += 1u;
+      coh.uprims += __ballot(La != f) == 0ull ? 1u : 0u;
+    }
+    prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, La, r, best_t, best, c_tri, c_sph, lp);
+    if (pb != La) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
+  }
+  if (STATS && next >= 0 && (uint32_t)next >= v.n_top) {
+    const int32_t f = __builtin_amdgcn_readfirstlane(next);
+    const bool uni = __ballot(next != f || (uint32_t)next < v.n_top) == 0ull;
+    ++coh.gnodes;
+    coh.unodes += uni ? 1u : 0u;
+  }
+  if (next < 0) return false;
+  if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS
+    const float4* __restrict__ t = v.top + kQuantNodeF4 * (uint32_t)next;
+    q = t;
+    qnode_load(t, w);
+  } else {
+    const float4* __restrict__ g = a.wnodes + (v.base + kQuantNodeF4 * (uint32_t)next);
+    q = g;
+    qnode_load(g, w);
+  }
+  return true;
+}
+
+// the suspended node of a wavefront / pool lane (re)loaded, in either format
+template <bool QN, class W>
+__device__ __forceinline__ void node_load(const float4* q, const WideView& v, W& w) {
+  if constexpr (QN) qnode_load(q, w);
+  else wide_load(q, v.sx, v.sy, v.sz, w);
+}
+
+// zrt_trace over compressed nodes (MODE 8): traverse_wide with wide_iter_q
+template <bool STATS, class StackT>
+__device__ __forceinline__ void traverse_wide_q(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
+                                                const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
+                                                int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
+                                                uint32_t& c_sph, uint32_t& c_replays, Coh& coh) {
+  const WideView v = wide_view(a, r, lds_top);
+  uint32_t sp = 0;
+  const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+  WideNodeQ w;
+  qnode_load(q, w);
+  while (wide_iter_q<STATS, StackT, true, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
+                                                c_sph, coh)) {
+  }
+  wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
 
 template <bool STATS, class StackT, bool PAXIS = ZRT_PAXIS_LOCK>
@@ -2371,7 +2639,7 @@ struct PoolLds {
 #ifndef ZRT_POOL_ATT_PATH
 #define ZRT_POOL_ATT_PATH 1
 #endif
-template <int PRNG, bool STATS, class StackT, bool GUARD>
+template <int PRNG, bool STATS, class StackT, bool GUARD, bool QN = false>
 __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the lane's traversal stack column
@@ -2435,10 +2703,10 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
       // shade once the queue is empty and fewer than 64 - wf_thresh lanes still traverse
       const uint32_t thresh = 64u - a.wf_thresh;
       WideView v{};
-      WideNode w;
+      std::conditional_t<QN, WideNodeQ, WideNode> w;
       if (trav) {
         v = wide_view(a, r, lds_top);
-        wide_load(q, v.sx, v.sy, v.sz, w);  // the suspended node (re)loaded
+        node_load<QN>(q, v, w);  // the suspended node (re)loaded
       }
       for (;;) {
         const uint64_t idle = __ballot(!trav);
@@ -2460,15 +2728,21 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
             sp = 0;
             v = wide_view(a, r, lds_top);
             q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
-            wide_load(q, v.sx, v.sy, v.sz, w);
+            node_load<QN>(q, v, w);
             trav = true;
           }
           const uint32_t n_idle = (uint32_t)__builtin_popcountll(idle);
           q_head += n_idle < avail ? n_idle : avail;
         }
         if (trav) {
-          if (!wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
-                                               c_sph, coh)) {
+          bool more;
+          if constexpr (QN)
+            more = wide_iter_q<STATS, StackT, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves,
+                                                          c_tri, c_sph, coh);
+          else
+            more = wide_iter<STATS, StackT, ZRT_POOL_SCALAR != 0, true, GUARD>(a, r, v, stk, gl, w, q, sp, best_t, best,
+                                                                               c_nodes, c_leaves, c_tri, c_sph, coh);
+          if (!more) {
             wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
             const uint32_t P = wave_paths + cp;
             pl.hit_t[P] = best_t;
@@ -2841,7 +3115,7 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
 #endif
 
 template <int MODE, int PRNG, bool STATS, class StackT>
-__global__ void __launch_bounds__(kBlock, MODE == 5 || MODE == 7 ? ZRT_WAVES_POOL
+__global__ void __launch_bounds__(kBlock, MODE == 5 || MODE == 7 || MODE == 8 || MODE == 9 ? ZRT_WAVES_POOL
                                           : MODE == 4 ? ZRT_WAVES_WF
                                           : MODE == 3 ? ZRT_WAVES_WIDE
                                           : MODE == 0 || MODE == 6 ? ZRT_WAVES_LIST
@@ -2850,6 +3124,8 @@ __global__ void __launch_bounds__(kBlock, MODE == 5 || MODE == 7 ? ZRT_WAVES_POO
   if constexpr (MODE == 6) render_loop_list<PRNG, STATS>(a);
   else if constexpr (MODE == 5) render_loop_pool<PRNG, STATS, StackT, false>(a);
   else if constexpr (MODE == 7) render_loop_pool<PRNG, STATS, StackT, true>(a);  // with the grazing-triangle guard
+  else if constexpr (MODE == 8) render_loop_pool<PRNG, STATS, StackT, false, true>(a);  // compressed nodes
+  else if constexpr (MODE == 9) render_loop_pool<PRNG, STATS, StackT, true, true>(a);   // compressed, guarded
   else if constexpr (MODE == 4) render_loop_wf<PRNG, STATS, StackT>(a);
   else render_loop<MODE, PRNG, STATS, StackT>(a);
 }
@@ -2872,8 +3148,8 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;
   float4* lds_top = reinterpret_cast<float4*>(lds_raw + a.lds_top_off);
-  if (MODE == 3 && !layout_ok(a)) return;
-  if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
+  if ((MODE == 3 || MODE == 8) && !layout_ok(a)) return;
+  if ((MODE == 3 || MODE == 8) && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const uint32_t gl = blockIdx.x * kBlock + threadIdx.x;
   if (gl >= n) return;
   const float* q = rays + 6ull * gl;
@@ -2899,6 +3175,11 @@ __global__ void __launch_bounds__(kBlock) trace_kernel(const KArgs a, const floa
     Coh coh;
     traverse_wide<false, StackT, true>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays,
                                        coh);
+  } else if (MODE == 8) {  // compressed nodes
+    uint32_t c_replays = 0;
+    Coh coh;
+    traverse_wide_q<false, StackT>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays,
+                                   coh);
   } else {
     traverse_bvh<MODE == 1, false>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph);
   }
@@ -3217,6 +3498,9 @@ struct zrt_ctx {
   uint32_t n_wide = 0, n_leaves = 0, wide_stack = 0, wide_stride = 0, n_top = 0, n_mats = 0;
   std::vector<uint32_t> slot_to_prim;  // device primitive slot -> reference list index
   zrt::DevBuf<float4> wnodes;
+  zrt::DevBuf<float4> qnodes, qleaves;  // compressed wide nodes + leaf records (q_ok)
+  bool q_ok = false;
+  uint32_t q_stride = 0;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
@@ -3257,6 +3541,7 @@ struct zrt_ctx {
   uint32_t last_tiles = 0, last_rank = 0, last_world = 1, last_tiles_x = 0, last_xbound = 0;
   bool last_stats = false;
   int last_mode = 0;
+  bool last_qn = false;  // the last launch read compressed nodes
   int last_loop = 0;  // zrt_stats::sampling_loop
   float last_guard = 0.0f;  // zrt_stats::guard
   int cu_count = 0;
@@ -3290,6 +3575,9 @@ struct HostScene {
   float guard = 0.0f;            // KArgs::guard
   std::vector<uint8_t> ref_sph;  // KArgs::ref_sph
   std::vector<float4> nodes, wn, prims, shade;
+  std::vector<float4> qn, ql;  // compressed wide nodes (8 octant copies) and leaf records, when q_ok
+  bool q_ok = false;
+  uint32_t q_stride = 0;       // float4s per octant copy of qn
   std::vector<DevMaterial> mats;
   std::vector<float> tex;
   std::vector<uint32_t> tex8;
@@ -3335,6 +3623,7 @@ float graze_leaf_margin() {  // ZRT_GRAZE_LEAF: leaf slots' coefficient (A/B of 
 
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
 // `device` >= 0: the GPU that may build the BVH (device_bvh).
+bool want_qnodes(uint32_t n_wide);
 void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
@@ -3474,6 +3763,22 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     std::memcpy(wn.data(), wide.nodes.data(), nw * sizeof(float4));
 #endif
     c->wide_stack = wide.max_stack + 3;  // + the dead entries of a branch-free push
+    // compressed nodes for trees past the caches (want_qnodes): the same tree, 64-B nodes
+    if (want_qnodes(wide.n_nodes)) {
+      const double tq = now_ms();
+      QuantWide qw = quantize_wide(wide);
+      if (qw.ok) {
+        c->qn.resize(qw.nodes.size());
+        std::memcpy(c->qn.data(), qw.nodes.data(), qw.nodes.size() * sizeof(float4));
+        c->ql.resize(std::max<size_t>(1, qw.leaves.size()));
+        std::memcpy(c->ql.data(), qw.leaves.data(), qw.leaves.size() * sizeof(float4));
+        c->q_ok = true;
+        c->q_stride = qw.n_nodes * kQuantNodeF4;
+      }
+      if (std::getenv("ZRT_DEBUG_LAUNCH"))
+        std::fprintf(stderr, "zrt preprocess: compressed nodes %s, %u leaf records, %.1f ms\n", qw.ok ? "built" : "refused",
+                     qw.n_leaves, now_ms() - tq);
+    }
     c->wn = std::move(wn);
     c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
@@ -3632,6 +3937,12 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   const double t1 = now_ms();
   c->nodes.upload(h.nodes);
   c->wnodes.upload(h.wn);
+  if (h.q_ok) {
+    c->qnodes.upload(h.qn);
+    c->qleaves.upload(h.ql);
+  }
+  c->q_ok = h.q_ok;
+  c->q_stride = h.q_stride;
   c->prims.upload(h.prims);
   c->shade.upload(h.shade);
   c->mats.upload(h.mats);
@@ -3696,6 +4007,13 @@ bool use_pool(const zrt_ctx* c, bool stk16) {
   (void)c;
   return !stk16;
 }
+// Compressed wide nodes (wide_iter_q, MODE 8 / 9) for this tree?  ZRT_QNODES=0/1
+// forces it; default: trees of the path-pool loop's size (>= 65536 wide nodes,
+// past the 16-bit stack), whose octant copies outgrow the caches.
+bool want_qnodes(uint32_t n_wide) {
+  if (const char* e = std::getenv("ZRT_QNODES")) return std::atoi(e) != 0;
+  return n_wide >= 65536;
+}
 // The list loop with per-lane work items (render_loop_list, MODE 6) for scenes
 // without a BVH; ZRT_LIST_LANES=0 forces the wave-unit loop (render_loop MODE 0).
 // C2: 34.1 (MODE 0, lanes in per-sample lockstep) -> 45.4 (MODE 0, free lanes
@@ -3721,6 +4039,8 @@ void* select_kernel_ps(int mode, bool stk16) {
   if (mode == 4) return stk16 ? kernel_ptr<4, PRNG, STATS, uint16_t>() : kernel_ptr<4, PRNG, STATS, uint32_t>();
   if (mode == 5) return stk16 ? kernel_ptr<5, PRNG, STATS, uint16_t>() : kernel_ptr<5, PRNG, STATS, uint32_t>();
   if (mode == 7) return stk16 ? kernel_ptr<7, PRNG, STATS, uint16_t>() : kernel_ptr<7, PRNG, STATS, uint32_t>();
+  if (mode == 8) return stk16 ? kernel_ptr<8, PRNG, STATS, uint16_t>() : kernel_ptr<8, PRNG, STATS, uint32_t>();
+  if (mode == 9) return stk16 ? kernel_ptr<9, PRNG, STATS, uint16_t>() : kernel_ptr<9, PRNG, STATS, uint32_t>();
   return stk16 ? kernel_ptr<2, PRNG, STATS, uint16_t>() : kernel_ptr<2, PRNG, STATS, uint32_t>();
 }
 #ifdef ZRT_ISA_KERNEL
@@ -3787,7 +4107,7 @@ uint32_t lane_state_words(uint32_t prng) {
 // The lockstep FAST loop (mode 3, neither wf nor pool) also holds its lane state
 // (ZRT_LANE_LDS) and keeps at most ZRT_STACK_ROWS_LOCK stack rows in LDS.
 LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth,
-                 bool wf, bool pool, uint32_t prng) {
+                 bool wf, bool pool, uint32_t prng, uint32_t node_f4 = 8) {
   const uint32_t waves = mode == 3 ? (pool ? ZRT_WAVES_POOL : wf ? ZRT_WAVES_WF : ZRT_WAVES_WIDE)
                          : mode == 0 ? ZRT_WAVES_LIST : ZRT_WAVES_PER_SIMD;
   // 256-thread blocks: `waves` blocks per CU; 1 KiB below the even share (a
@@ -3795,7 +4115,7 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
   const size_t budget = (160u << 10) / waves - (1u << 10);
   const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
   const size_t row_att = sizeof(uint32_t) * (pool ? kBlockPaths : kBlock);  // one att code per lane / path
-  const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(n_top) * 8 * sizeof(float4) * kOctCopies : 0;
+  const size_t top = mode == 3 && ZRT_LDS_TOP ? size_t(n_top) * node_f4 * sizeof(float4) * kOctCopies : 0;
   const size_t pool_b = pool ? kPoolLdsBytes : 0;
   const bool lock = mode == 3 && !wf && !pool;
   const size_t state = lock && ZRT_LANE_LDS ? size_t(lane_state_words(prng)) * sizeof(uint32_t) * kBlock : 0;
@@ -3856,8 +4176,8 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
   return L;
 }
 LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf, bool pool,
-                 uint32_t prng) {
-  return plan_lds(c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf, pool, prng);
+                 uint32_t prng, uint32_t node_f4 = 8) {
+  return plan_lds(c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf, pool, prng, node_f4);
 }
 
 // Longest-processing-time-first order of this rank's tiles (zrt.h,
@@ -3894,6 +4214,33 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.tile_order = nullptr;
   const uint32_t pgrid = std::max(1u, std::min(grid, (my_tiles + kBlock / 64 - 1) / (kBlock / 64)));
   pa.n_lanes = pgrid * kBlock;
+  // the probe is the lockstep loop over the full nodes, whatever loop and node
+  // format the render launch uses: its own LDS plan (the render's may be the path
+  // pool's, whose regions the lockstep loop would read as its lane state and rows)
+  const LdsPlan pp = plan_lds(c, 3, stk16, a.stack_depth, a.max_depth, false, false, prng, 8);
+  pa.wnodes = c->wnodes.p;
+  pa.wide_stride = c->wide_stride;
+  pa.node_f4 = 8;
+  pa.qleaves = nullptr;
+  pa.lds_rows = pp.stack_rows;
+  pa.lds_top_off = pp.top_off;
+  pa.lds_att_off = pp.att_off;
+  pa.att_lds_rows = pp.att_rows;
+  pa.lds_mat_off = pp.mat_off;
+  pa.mats_in_lds = pp.mats_in_lds;
+  pa.lds_pool_off = pp.pool_off;
+  pa.lds_state_off = pp.state_off;
+  lds = pp.bytes;
+  if (a.stack_depth > pp.stack_rows) {  // its deep stack rows (the render launch's buffer, grown if need be)
+    const uint64_t need = uint64_t(a.stack_depth - pp.stack_rows) * pa.n_lanes * (stk16 ? 2u : 4u);
+    if (c->stack_ovf.n < need) {
+      HIPCHK(hipStreamSynchronize(st));  // (the previous launch may still read the old buffer)
+      c->stack_ovf.alloc(need);
+    }
+    a.stack_ovf = pa.stack_ovf = c->stack_ovf.p;
+  }
+  // the global attenuation rows: the render launch's buffer holds the probe's rows
+  // (fewer lanes, at least as many LDS rows: zrt_ctx_render_tiles sizes it)
   HIPCHK(hipMemsetAsync(c->probe_scratch.p, 0, kScratchSlots * sizeof(unsigned long long), st));
   void* fn = prng == ZRT_PRNG_XOSHIRO256 ? probe_ptr<ZRT_PRNG_XOSHIRO256>(stk16)
                                          : probe_ptr<ZRT_PRNG_XOROSHIRO128>(stk16);
@@ -4176,21 +4523,24 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // the grazing-triangle guard (ZRT_FLAG_GUARD): carried by the path-pool loop's traversal
     const bool guard_on = mode == 3 && (p->flags & ZRT_FLAG_GUARD) != 0 && c->guard > 0.0f;
     const bool pool = mode == 3 && p->max_depth >= 1 && (zrt::use_pool(c, stk16) || guard_on);
+    // the path pool over compressed nodes (MODE 8 / 9) where the context built them
+    const bool qn = pool && c->q_ok;
+    const uint32_t node_f4 = qn ? zrt::kQuantNodeF4 : 8u;
     if (pool && stk16) {
       const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
-      const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * 8 * sizeof(float4) * zrt::kOctCopies : 0;
+      const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * node_f4 * sizeof(float4) * zrt::kOctCopies : 0;
       if (size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) + top + zrt::kPoolLdsBytes > budget) stk16 = false;
     }
     const bool list_lanes = mode == 0 && zrt::use_list_lanes();
     // (the guard's branch costs the path pool 0.7 % on C5, so a guarded render has a
     // kernel of its own, MODE 7; profiles/r04/r04n)
-    const int kmode = pool ? (guard_on ? 7 : 5) : wf ? 4 : list_lanes ? 6 : mode;
+    const int kmode = pool ? (qn ? (guard_on ? 9 : 8) : (guard_on ? 7 : 5)) : wf ? 4 : list_lanes ? 6 : mode;
     void* kfn = zrt::select_kernel(kmode, p->prng, diag, stk16);
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng);
+    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng, node_f4);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
     int per_cu = 0;
@@ -4273,8 +4623,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
                                 std::fabs(a.org[2] - a.root_c[2])});
       a.check_origins = m <= a.origin_bound ? 0u : 1u;
     }
-    a.wnodes = c->wnodes.p;
-    a.wide_stride = c->wide_stride;
+    a.wnodes = qn ? c->qnodes.p : c->wnodes.p;
+    a.wide_stride = qn ? c->q_stride : c->wide_stride;
+    a.node_f4 = node_f4;
+    a.qleaves = qn ? c->qleaves.p : nullptr;
     a.lds_rows = lds_rows;
     if (stack_depth > lds_rows) {
       const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
@@ -4362,7 +4714,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     c->last_xbound = g.xbound;
     c->last_stats = diag;
     c->last_mode = mode;
-    c->last_loop = kmode == 7 ? 5 : kmode;
+    c->last_loop = kmode == 7 || kmode == 8 || kmode == 9 ? 5 : kmode;
+    c->last_qn = qn;
     c->last_guard = a.guard;
     c->launched = 1;
     return ZRT_OK;
@@ -4406,7 +4759,8 @@ int zrt_ctx_stats(zrt_ctx* c, zrt_stats* out) {
     std::memcpy(&out->box_excess_max_triangle, &bt, 4);
     std::memcpy(&out->box_excess_max_sphere, &bs, 4);
     out->box_excess_hits = h[zrt::kExcessHits];
-    out->node_bytes = c->last_mode == 3 ? 128 : 32;  // FAST: leaf boxes ride in their parent's 128 B
+    // FAST: leaf boxes ride in their parent's 128 B; compressed: 64-B nodes (+ 32-B leaf records)
+    out->node_bytes = c->last_mode == 3 ? (c->last_qn ? 64 : 128) : 32;
     out->wide_nodes = c->n_wide;
     out->sampling_loop = uint32_t(c->last_loop);
     out->guard = c->last_guard;
@@ -4842,7 +5196,11 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
     const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows : c->n_nodes < 65536;
     const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
-    const zrt::LdsPlan lp = zrt::plan_lds(c.get(), mode, stk16, stack_depth, 0, false, false, ZRT_PRNG_XOROSHIRO128);
+    // FAST over compressed nodes (wide_iter_q, MODE 8) where the context built them
+    const bool qn = mode == 3 && c->q_ok;
+    const uint32_t node_f4 = qn ? zrt::kQuantNodeF4 : 8u;
+    const zrt::LdsPlan lp = zrt::plan_lds(c.get(), mode, stk16, stack_depth, 0, false, false, ZRT_PRNG_XOROSHIRO128,
+                                          node_f4);
     const uint32_t lds_rows = lp.stack_rows;
     const uint32_t grid = (n_rays + zrt::kBlock - 1) / zrt::kBlock;
     const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
@@ -4857,8 +5215,10 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.nodes = c->nodes.p;
     a.prims = c->prims.p;
     a.shade = c->shade.p;
-    a.wnodes = c->wnodes.p;
-    a.wide_stride = c->wide_stride;
+    a.wnodes = qn ? c->qnodes.p : c->wnodes.p;
+    a.wide_stride = qn ? c->q_stride : c->wide_stride;
+    a.node_f4 = node_f4;
+    a.qleaves = qn ? c->qleaves.p : nullptr;
     a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
@@ -4897,7 +5257,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
 #ifdef ZRT_ISA_KERNEL
     fn = nullptr;
 #else
-    fn = mode == 0 ? ZRT_TK(0) : mode == 1 ? ZRT_TK(1) : mode == 2 ? ZRT_TK(2) : ZRT_TK(3);
+    fn = mode == 0 ? ZRT_TK(0) : mode == 1 ? ZRT_TK(1) : mode == 2 ? ZRT_TK(2) : qn ? ZRT_TK(8) : ZRT_TK(3);
 #endif
 #undef ZRT_TK
     const float* rp = d_rays.p;
@@ -4965,11 +5325,14 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
         for (bool stk16 : {true, false}) {
           for (uint32_t prng : {uint32_t(ZRT_PRNG_XOROSHIRO128), uint32_t(ZRT_PRNG_XOSHIRO256)}) {
             for (uint32_t depth : {0u, 1u, 2u, 5u, 20u, 50u}) {
-              const uint32_t sd = mode == 3 ? std::max(h.wide_stack, ref_depth) : ref_depth;
-              where = "mode " + std::to_string(mode) + " loop " + std::to_string(loop) + " stk16 " +
-                      std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " + std::to_string(depth);
-              (void)zrt::plan_lds(h.n_top, n_mats, mode, stk16, sd, depth, loop == 1, loop == 2, prng);
-              ++*n_checked;
+              for (uint32_t nf4 : {8u, 4u}) {  // full / compressed wide nodes (the path pool only)
+                if (nf4 == 4u && loop != 2) continue;
+                const uint32_t sd = mode == 3 ? std::max(h.wide_stack, ref_depth) : ref_depth;
+                where = "mode " + std::to_string(mode) + " loop " + std::to_string(loop) + " stk16 " +
+                        std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " + std::to_string(depth);
+                (void)zrt::plan_lds(h.n_top, n_mats, mode, stk16, sd, depth, loop == 1, loop == 2, prng, nf4);
+                ++*n_checked;
+              }
             }
           }
         }
