@@ -2909,6 +2909,117 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
   }
 }
 
+#ifndef ZRT_LIST_MERGE
+#define ZRT_LIST_MERGE 1  // list loop: one unit() per step for every new direction (scatters and camera rays)
+#endif
+// shade_step's first half for the list loop (ZRT_LIST_MERGE): a hit's scatter up
+// to the direction it normalises.  Every material's new direction - and a new
+// sample's camera ray - is normalised once per step for all lanes together
+// (unit(), vector.zig:88-92, ~20 VALU: where the materials ran it in their own
+// branches a wave paid for it up to six times per step), and a metal scatter's
+// absorption test (material.zig:96-101) reads the normalised direction after it.
+// Same operations on the same values as shade_step, in the same order per lane.
+// pend: 0 nothing to normalise, 1 a scatter, 2 a metal scatter to be tested after.
+template <bool STATS, class R>
+__device__ __forceinline__ void shade_hit_a(const KArgs& a, const DevMaterial* __restrict__ mats, R& rng, int best,
+                                            float best_t, const V3 o, const V3 d, bool& path_end, bool& sky, V3& L,
+                                            uint32_t& c_bg, uint32_t& c_shade, uint32_t& c_tex, V3& x, V3& loc,
+                                            V3& normal, uint32_t& att, uint32_t& pend) {
+  pend = 0;
+  if (best < 0) {
+    ++c_bg;
+    L = background(d);
+    path_end = true;
+    sky = true;
+    return;
+  }
+  float4 sh;
+  const int fb = __builtin_amdgcn_readfirstlane(best);
+  if (ZRT_SCALAR_PRIMS && __ballot(best != fb) == 0ull) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float4 cfloat4;
+    sh = ((cfloat4*)a.shade)[fb];
+#else
+    sh = a.shade[fb];
+#endif
+  } else {
+    sh = a.shade[best];
+  }
+  const uint32_t tag = __float_as_uint(sh.w);
+  const MatReg mat = load_material(mats, tag & 0x7fffffffu);
+  const uint32_t mkind = mat.kind();
+  const bool need_uv = mkind != ZRT_MAT_DIELECTRIC && mat.tex_kind() == ZRT_TEX_IMAGE;
+  if (STATS) {
+    ++c_shade;
+    c_tex += need_uv ? 1u : 0u;
+  }
+  loc = add(o, scale(d, best_t));
+  V3 outward;
+  float tu = 0.0f, tv = 0.0f;
+  if (tag >> 31) {
+    outward = mk(sh.x, sh.y, sh.z);
+    if (need_uv) {
+      const float4 p0 = a.prims[3 * best + 0];
+      const float4 p1 = a.prims[3 * best + 1];
+      const float4 p2 = a.prims[3 * best + 2];
+      const V3 n = mk(p2.y, p2.z, p2.w);
+      const float det = -dot(d, n);
+      const float inv_det = inv_det_rn(det, a.tri_rcp_fast);
+      const V3 ao = mk(o.x - p0.x, o.y - p0.y, o.z - p0.z);
+      const V3 dao = cross(ao, d);
+      tu = dot(mk(p1.z, p1.w, p2.x), dao) * inv_det;
+      tv = -dot(mk(p0.w, p1.x, p1.y), dao) * inv_det;
+    }
+  } else {
+    const float4 c = a.prims[3 * best];
+    outward = scale(sub(loc, mk(c.x, c.y, c.z)), sh.x);
+    if (need_uv) {
+      const float theta = dev::acos_z(-outward.y);
+      const float phi = dev::atan2_z(-outward.z, -outward.x) + kPi;
+      tu = dev::div_known(phi, kTwoPi, kInvTwoPi);
+      tv = dev::div_known(theta, kPi, kInvPi);
+    }
+  }
+  bool front = true;
+  normal = outward;
+  if (dot(d, outward) > 0.0f) {
+    normal = neg(outward);
+    front = false;
+  }
+  // metal and dielectric both start from unit(d): one normalisation for the lanes of either
+  V3 ud = d;
+  if (mkind != ZRT_MAT_LAMBERTIAN) ud = unit(d);
+  if (mkind == ZRT_MAT_LAMBERTIAN) {
+    const float r1 = rand_float(rng);
+    const float r2 = rand_float(rng);
+    const float rr = dev::sqrt_rn(1.0f - r1 * r1);
+    float sn, cs;
+    dev::sincos_z(kTwoPi * r2, &sn, &cs);
+    V3 hv = mk(cs * rr, sn * rr, r1);
+    if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
+    x = add(normal, hv);
+    att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);
+    pend = 1;
+  } else if (mkind == ZRT_MAT_METAL) {
+    x = reflect(ud, normal);
+    att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);  // (used only when the scatter is not absorbed)
+    pend = 2;
+  } else {
+    const float ratio = front ? dev::rcp_rn(mat.ior()) : mat.ior();
+    const float cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+    const float sin_theta = dev::sqrt_rn(1.0f - cos_theta * cos_theta);
+    bool refl = ratio * sin_theta > 1.0f;
+    if (!refl) {
+      const float r0 = dev::div_rn(1.0f - ratio, 1.0f + ratio);
+      const float reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+      refl = reflectance > rand_float(rng);
+    }
+    x = refl ? reflect(ud, normal) : refract(ud, normal, ratio);
+    att = kAttOne;
+    pend = 1;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // The surface-list loop with per-lane work items (MODE 6; raytrace.zig:71-81
 // without a BVH, config C2).  Every ray of a list scene costs the same - all
@@ -3032,6 +3143,9 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
     bool path_end = false, sky = false;
     V3 L = mk(0.0f, 0.0f, 0.0f);
     const uint32_t dh0 = c_depth, rf0 = c_refl, bg0 = c_bg;
+    const AttRows ar{att_l, kBlock, gl, a.n_lanes};
+    V3 x = mk(0.0f, 0.0f, 0.0f), loc = x, nrm = x;  // ZRT_LIST_MERGE: the direction to normalise, hit, normal
+    uint32_t att = 0, pend = 0;
     if (depth_left == 0) {
       ++c_depth;
       path_end = true;
@@ -3057,16 +3171,16 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
           sphere_test<false>(cprims[3 * i], (int)i, r, best_t, best);
         }
       }
-      shade_step<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, rng, best, best_t, o, d, depth_left, path_end,
-                        sky, L, c_bg, c_refl, c_shade, c_tex, coh);
+      if (ZRT_LIST_MERGE)
+        shade_hit_a<STATS>(a, mats, rng, best, best_t, o, d, path_end, sky, L, c_bg, c_shade, c_tex, x, loc, nrm, att,
+                           pend);
+      else
+        shade_step<STATS>(a, mats, ar, rng, best, best_t, o, d, depth_left, path_end, sky, L, c_bg, c_refl, c_shade,
+                          c_tex, coh);
     }
-    if (a.scanlines) {  // this lane's item is one pixel: its events go to its row (raytrace.zig:184)
-      scanline_add(a, py, 0, c_depth - dh0);
-      scanline_add(a, py, 1, c_refl - rf0);
-      scanline_add(a, py, 2, c_bg - bg0);
-    }
+    bool cam = false;  // ZRT_LIST_MERGE: the item's next sample starts in this step
     if (path_end) {
-      const V3 col = sky ? att_product<STATS>(a, mats, AttRows{att_l, kBlock, gl, a.n_lanes}, a.max_depth - depth_left, L, coh) : L;
+      const V3 col = sky ? att_product<STATS>(a, mats, ar, a.max_depth - depth_left, L, coh) : L;
       acc_r += col.x;
       acc_g += col.y;
       acc_b += col.z;
@@ -3074,7 +3188,53 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
       if (++sample == s_end) {  // the chunk's sequential sum, in its [chunk][pixel slot] place
         a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
         has = false;
+      } else if (ZRT_LIST_MERGE) {  // the next sample's jitter + Camera.getRay (raytrace.zig:173-175)
+        const uint64_t offset = (uint64_t)py * a.width + px;
+        rng.init(((offset << 16) | (uint64_t)sample) + a.seed_mix);
+        const float u = dev::div_known((float)px + rand_float(rng) - 0.5f, a.f_width, a.inv_width);
+        const float v = dev::div_known((float)py + rand_float(rng) - 0.5f, a.f_height, a.inv_height);
+        x = sub(add(add(mk(a.llc[0], a.llc[1], a.llc[2]), scale(mk(a.hor[0], a.hor[1], a.hor[2]), u)),
+                    scale(mk(a.ver[0], a.ver[1], a.ver[2]), v)),
+                mk(a.org[0], a.org[1], a.org[2]));
+        cam = true;
+        in_sample = true;
       }
+    }
+    if (ZRT_LIST_MERGE && (pend != 0u || cam)) {  // every new direction of the step, normalised together
+      const V3 nd = unit(x);
+      if (cam) {
+        o = mk(a.org[0], a.org[1], a.org[2]);
+        d = nd;
+        depth_left = a.max_depth;
+      } else if (pend == 1u || dot(nd, nrm) > 0.0f) {  // scattered (material.zig:71-128)
+        ++c_refl;
+        if (depth_left > 1) {  // (shade_step: an attenuation pushed at depth 1 is never read)
+          const uint32_t i = a.max_depth - depth_left;
+          if (i < a.att_lds_rows) {
+            ar.lds[i * ar.lds_stride] = att;
+          } else {
+            a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = att;
+            if (STATS) ++coh.attw;
+          }
+        }
+        o = loc;
+        d = nd;
+        --depth_left;
+      } else {  // a metal scatter absorbed: the path ends black (its next sample starts next step)
+        acc_r += 0.0f;
+        acc_g += 0.0f;
+        acc_b += 0.0f;
+        in_sample = false;
+        if (++sample == s_end) {
+          a.partial[slot] = make_float4(acc_r, acc_g, acc_b, 0.0f);
+          has = false;
+        }
+      }
+    }
+    if (a.scanlines) {  // this lane's item is one pixel: its events go to its row (raytrace.zig:184)
+      scanline_add(a, py, 0, c_depth - dh0);
+      scanline_add(a, py, 1, c_refl - rf0);
+      scanline_add(a, py, 2, c_bg - bg0);
     }
   }
   if (!a.scanlines) {  // (with ZRT_FLAG_SCANLINES they went to the frame rows, whose sums are the totals)
