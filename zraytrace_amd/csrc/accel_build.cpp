@@ -270,6 +270,7 @@ WideBvh build_wide_bvh(const std::vector<RefLeaf>& leaves, uint32_t top_levels, 
         }
       }
       level.swap(below);
+      out.level_end.push_back(uint32_t(next_pos));
     }
     out.n_top = uint32_t(next_pos);
     for (const int32_t r : level) {

@@ -29,6 +29,7 @@ struct WideBvh {
   std::vector<float4v> nodes;   // 8 per wide node, node 0 = root
   uint32_t n_nodes = 0, n_leaves = 0, depth = 0, max_stack = 0;
   uint32_t n_top = 0;           // nodes of the top levels, stored first (0 .. n_top-1)
+  std::vector<uint32_t> level_end;  // nodes of the first 1, 2, .. top levels (breadth-first prefix)
   uint32_t layout = 0;          // kLayout* bits of this encoding
 };
 

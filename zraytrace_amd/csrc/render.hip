@@ -3660,7 +3660,7 @@ struct zrt_ctx {
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> qnodes, qleaves;  // compressed wide nodes + leaf records (q_ok)
   bool q_ok = false;
-  uint32_t q_stride = 0;
+  uint32_t q_stride = 0, q_top = 0;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
@@ -3738,6 +3738,7 @@ struct HostScene {
   std::vector<float4> qn, ql;  // compressed wide nodes (8 octant copies) and leaf records, when q_ok
   bool q_ok = false;
   uint32_t q_stride = 0;       // float4s per octant copy of qn
+  uint32_t q_top = 0;          // compressed nodes served from LDS (their top levels)
   std::vector<DevMaterial> mats;
   std::vector<float> tex;
   std::vector<uint32_t> tex8;
@@ -3784,6 +3785,7 @@ float graze_leaf_margin() {  // ZRT_GRAZE_LEAF: leaf slots' coefficient (A/B of 
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
 // `device` >= 0: the GPU that may build the BVH (device_bvh).
 bool want_qnodes(uint32_t n_wide);
+uint32_t qtop_levels();
 void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
@@ -3902,8 +3904,14 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     c->graze_m = graze_margin();
     c->graze_leaf = std::max(c->graze_m, graze_leaf_margin());
     c->guard = 0.0f;  // (set below, once the triangles are known)
-    const WideBvh wide = build_wide_bvh(leaves, 2, ZRT_GROW ? 0.5f * c->graze_m : 0.0f, ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f,
-                                          ZRT_SPHERE_SLOTS != 0);
+    // the top levels stored first (LDS): two for the full 128-B nodes; a tree that
+    // also gets compressed nodes stores qtop_levels() (their 64-B nodes leave room
+    // for a third level in the path pool's LDS), the full kernels reading the first two
+    const uint32_t n_leaf_est = uint32_t(leaves.size());
+    const bool want_q = want_qnodes((n_leaf_est + 2) / 3);  // (the wide tree has about leaves / 3 nodes)
+    const uint32_t top_levels = want_q ? qtop_levels() : 2u;
+    const WideBvh wide = build_wide_bvh(leaves, top_levels, ZRT_GROW ? 0.5f * c->graze_m : 0.0f,
+                                        ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f, ZRT_SPHERE_SLOTS != 0);
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt preprocess: wide tree %u nodes in %.1f ms\n", wide.n_nodes, now_ms() - tw);
     const size_t nw = wide.nodes.size();
@@ -3924,7 +3932,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
 #endif
     c->wide_stack = wide.max_stack + 3;  // + the dead entries of a branch-free push
     // compressed nodes for trees past the caches (want_qnodes): the same tree, 64-B nodes
-    if (want_qnodes(wide.n_nodes)) {
+    if (want_q) {
       const double tq = now_ms();
       QuantWide qw = quantize_wide(wide);
       if (qw.ok) {
@@ -3934,6 +3942,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
         std::memcpy(c->ql.data(), qw.leaves.data(), qw.leaves.size() * sizeof(float4));
         c->q_ok = true;
         c->q_stride = qw.n_nodes * kQuantNodeF4;
+        c->q_top = wide.n_top;
       }
       if (std::getenv("ZRT_DEBUG_LAUNCH"))
         std::fprintf(stderr, "zrt preprocess: compressed nodes %s, %u leaf records, %.1f ms\n", qw.ok ? "built" : "refused",
@@ -3943,7 +3952,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     c->wide_stride = uint32_t(nw);
     c->n_wide = wide.n_nodes;
     c->n_leaves = wide.n_leaves;
-    c->n_top = wide.n_top;
+    c->n_top = wide.level_end.empty() ? 0u : wide.level_end[std::min<size_t>(2, wide.level_end.size()) - 1];
     c->layout = wide.layout;
     if (const char* e = std::getenv("ZRT_DEBUG_TREE_LAYOUT"))  // tests: a tree another kernel would have to decode
       c->layout ^= uint32_t(std::strtoul(e, nullptr, 0));
@@ -4103,6 +4112,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   }
   c->q_ok = h.q_ok;
   c->q_stride = h.q_stride;
+  c->q_top = h.q_top;
   c->prims.upload(h.prims);
   c->shade.upload(h.shade);
   c->mats.upload(h.mats);
@@ -4173,6 +4183,13 @@ bool use_pool(const zrt_ctx* c, bool stk16) {
 bool want_qnodes(uint32_t n_wide) {
   if (const char* e = std::getenv("ZRT_QNODES")) return std::atoi(e) != 0;
   return n_wide >= 65536;
+}
+// Top levels of a compressed tree served from LDS (ZRT_QTOP overrides): every ray
+// reads the root and a level-1 node, most a level-2 node - with 64-B nodes the
+// third level (<= 21 nodes, 10.5 KiB of octant copies) fits beside the pool's queues
+uint32_t qtop_levels() {
+  if (const char* e = std::getenv("ZRT_QTOP")) return uint32_t(std::max(1, std::min(4, std::atoi(e))));
+  return 3;
 }
 // The list loop with per-lane work items (render_loop_list, MODE 6) for scenes
 // without a BVH; ZRT_LIST_LANES=0 forces the wave-unit loop (render_loop MODE 0).
@@ -4337,7 +4354,8 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
 }
 LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, uint32_t max_depth, bool wf, bool pool,
                  uint32_t prng, uint32_t node_f4 = 8) {
-  return plan_lds(c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf, pool, prng, node_f4);
+  return plan_lds(node_f4 == kQuantNodeF4 ? c->q_top : c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf,
+                  pool, prng, node_f4);
 }
 
 // Longest-processing-time-first order of this rank's tiles (zrt.h,
@@ -4688,7 +4706,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const uint32_t node_f4 = qn ? zrt::kQuantNodeF4 : 8u;
     if (pool && stk16) {
       const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
-      const size_t top = ZRT_LDS_TOP ? size_t(c->n_top) * node_f4 * sizeof(float4) * zrt::kOctCopies : 0;
+      const size_t top = ZRT_LDS_TOP ? size_t(qn ? c->q_top : c->n_top) * node_f4 * sizeof(float4) * zrt::kOctCopies : 0;
       if (size_t(stack_depth) * zrt::kBlock * sizeof(uint16_t) + top + zrt::kPoolLdsBytes > budget) stk16 = false;
     }
     const bool list_lanes = mode == 0 && zrt::use_list_lanes();
@@ -4794,7 +4812,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       a.stack_ovf = c->stack_ovf.p;
     }
     a.n_lanes = uint32_t(n_lanes);
-    a.n_top = c->n_top;
+    a.n_top = qn ? c->q_top : c->n_top;
     a.lds_top_off = lp.top_off;
     a.lds_att_off = lp.att_off;
     a.att_lds_rows = lp.att_rows;
@@ -4808,7 +4826,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     if (std::getenv("ZRT_DEBUG_LAUNCH"))
       std::fprintf(stderr, "zrt launch: mode %d stk16 %d grid %u (%d blocks/CU x %d CUs) lds %zu B "
                    "(stack rows %u, top nodes %u @%u, att rows %u @%u, mats %u @%u)\n", mode, int(stk16), grid,
-                   per_cu, c->cu_count, lds, lp.stack_rows, c->n_top, lp.top_off, lp.att_rows, lp.att_off,
+                   per_cu, c->cu_count, lds, lp.stack_rows, a.n_top, lp.top_off, lp.att_rows, lp.att_off,
                    lp.mats_in_lds ? c->n_mats : 0u, lp.mat_off);
     a.chunk = chunk;
     a.n_chunks = n_chunks;
@@ -5403,7 +5421,7 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.guard = std::getenv("ZRT_DEBUG_NO_GUARD") ? 0.0f : c->guard;
     a.lds_rows = lds_rows;
     a.n_lanes = uint32_t(n_lanes);
-    a.n_top = c->n_top;
+    a.n_top = qn ? c->q_top : c->n_top;
     a.lds_top_off = lp.top_off;
     a.lds_att_off = lp.att_off;
     if (stack_depth > lds_rows) {
@@ -5490,7 +5508,8 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
                 const uint32_t sd = mode == 3 ? std::max(h.wide_stack, ref_depth) : ref_depth;
                 where = "mode " + std::to_string(mode) + " loop " + std::to_string(loop) + " stk16 " +
                         std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " + std::to_string(depth);
-                (void)zrt::plan_lds(h.n_top, n_mats, mode, stk16, sd, depth, loop == 1, loop == 2, prng, nf4);
+                (void)zrt::plan_lds(nf4 == 4u ? h.q_top : h.n_top, n_mats, mode, stk16, sd, depth, loop == 1,
+                                    loop == 2, prng, nf4);
                 ++*n_checked;
               }
             }
