@@ -502,6 +502,14 @@ int zrt_debug_division(uint64_t n, uint64_t* counts, uint32_t device);
  * share).  n_checked: the number of plans checked.  ZRT_E_UNSUPPORTED names the
  * first violation. */
 int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked);
+/* Host-side check of the compressed wide nodes built for this scene (no device
+ * needed): every plane of every node's eight octant copies decodes exactly to
+ * an f32, every slot's decoded box contains the full node's box of that slot,
+ * near / far bytes are the full node's min / max in the octant's order, and
+ * every leaf slot's record holds the full node's leaf box and primitive refs bit
+ * for bit.  n_checked: the slots checked.  ZRT_E_UNSUPPORTED names the first
+ * violation (or a tree the encoder refused). */
+int zrt_debug_qnodes(const zrt_scene* scene, uint64_t* n_checked);
 
 #ifdef __cplusplus
 }

@@ -326,3 +326,15 @@ def test_lds_plans_disjoint(scenes, index):
     n = z.debug_lds_plans(scenes(index))
     # modes 0-2 one loop each, mode 3 lockstep / wavefront / pool (full and compressed nodes); x stk16 x prng x depth
     assert n == (1 + 1 + 1 + 1 + 1 + 2) * 2 * 2 * 6
+
+
+@pytest.mark.parametrize("index", [0, 2, 3, 4])
+def test_compressed_nodes_encode_the_full_tree(scenes, index):
+    """accel_build.hpp quantize_wide (DESIGN.md §3 "Compressed nodes"), on CPU: in
+    every octant copy every plane decodes exactly, every slot's quantized box
+    contains the full node's box, inner refs are the full node's, and every leaf
+    record holds the reference leaf's box and primitive refs bit for bit - what
+    wide_iter_q relies on to take wide_iter's decisions."""
+    s = scenes(index)
+    n = z.debug_qnodes(s)
+    assert n >= 8 * 4 * 100  # 8 octant copies x 4 slots x the tree's nodes

@@ -438,3 +438,12 @@ def debug_lds_plans(scene) -> int:
     n = C.c_uint32()
     check(lib().zrt_debug_lds_plans(view, C.byref(n)))
     return n.value
+
+
+def debug_qnodes(scene) -> int:
+    """Host-side check of the scene's compressed wide nodes (zrt_debug_qnodes; no
+    device): returns the number of slots checked, raises ZrtError on a violation."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    n = C.c_uint64()
+    check(lib().zrt_debug_qnodes(view, C.byref(n)))
+    return n.value

@@ -178,6 +178,7 @@ SIGNATURES = [
                                 C.c_uint32, C.c_uint32]),
     ("zrt_debug_division", C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32]),
     ("zrt_debug_lds_plans", C.c_int, [C.POINTER(Scene), C.POINTER(C.c_uint32)]),
+    ("zrt_debug_qnodes", C.c_int, [C.POINTER(Scene), C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None

@@ -69,6 +69,7 @@ struct KArgs {
   const float4* __restrict__ shade;
   const float4* __restrict__ wnodes;   // FAST: 4-wide nodes (node_f4 float4 each: 8 full, 4 compressed)
   const float4* __restrict__ qleaves;  // compressed nodes' leaf records (kLeafRecF4 float4 each), else null
+  uint32_t n_qnodes, n_qleaves;        // compressed nodes per octant copy and leaf records (bounds checks)
   const DevMaterial* __restrict__ mats;
   const float* __restrict__ texels;    // f32 RGB images
   const uint32_t* __restrict__ texels8;  // 8-bit RGBX images (every value exactly k/255)
@@ -1548,7 +1549,7 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
   (void)q;
   const int stride = kBlock;
   const uint32_t cap = a.stack_depth;
-  const uint32_t rows = sizeof(StackT) == 4 ? a.lds_rows : cap;
+  const uint32_t rows = a.lds_rows;  // the first rows in LDS, the rest in global memory (either stack width)
   StackT* __restrict__ ovf = reinterpret_cast<StackT*>(a.stack_ovf) + gl;
   const float inf = __builtin_inff();
   const bool sx = v.sx, sy = v.sy, sz = v.sz;
@@ -1688,6 +1689,10 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
     const int ref = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
     const bool sph = ref < -kSphereSlotBias;
     const uint32_t L = (uint32_t)(-(sph ? ref + kSphereSlotBias : ref) - 1);
+    if (__builtin_expect(L >= a.n_qleaves, 0)) {  // a corrupt ref: report, never read past the records
+      atomicOr(a.error_flag, kErrLayout);
+      continue;
+    }
     const float4 mn = a.qleaves[2 * L], mx = a.qleaves[2 * L + 1];
     const float bx = sx ? mx.x : mn.x, cx = sx ? mn.x : mx.x;
     const float by = sy ? mx.y : mn.y, cy = sy ? mn.y : mx.y;
@@ -1725,6 +1730,10 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
     coh.unodes += uni ? 1u : 0u;
   }
   if (next < 0) return false;
+  if (__builtin_expect((uint32_t)next >= a.n_qnodes, 0)) {  // a corrupt node index: report, never read past the tree
+    atomicOr(a.error_flag, kErrLayout);
+    return false;
+  }
   if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS
     const float4* __restrict__ t = v.top + kQuantNodeF4 * (uint32_t)next;
     q = t;
@@ -3660,7 +3669,7 @@ struct zrt_ctx {
   zrt::DevBuf<float4> wnodes;
   zrt::DevBuf<float4> qnodes, qleaves;  // compressed wide nodes + leaf records (q_ok)
   bool q_ok = false;
-  uint32_t q_stride = 0, q_top = 0;
+  uint32_t q_stride = 0, q_top = 0, n_qleaves = 0;
   zrt::DevBuf<float4> nodes, prims, shade;
   zrt::DevBuf<zrt::DevMaterial> mats;
   zrt::DevBuf<float> texels;
@@ -4113,6 +4122,7 @@ void upload_scene(zrt_ctx* c, const HostScene& h) {
   c->q_ok = h.q_ok;
   c->q_stride = h.q_stride;
   c->q_top = h.q_top;
+  c->n_qleaves = uint32_t(h.ql.size() / kLeafRecF4);
   c->prims.upload(h.prims);
   c->shade.upload(h.shade);
   c->mats.upload(h.mats);
@@ -4399,7 +4409,9 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.wnodes = c->wnodes.p;
   pa.wide_stride = c->wide_stride;
   pa.node_f4 = 8;
+  pa.n_top = c->n_top;  // (the full nodes' top levels: a compressed tree keeps more in LDS)
   pa.qleaves = nullptr;
+  pa.n_qnodes = pa.n_qleaves = 0;
   pa.lds_rows = pp.stack_rows;
   pa.lds_top_off = pp.top_off;
   pa.lds_att_off = pp.att_off;
@@ -4805,6 +4817,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.wide_stride = qn ? c->q_stride : c->wide_stride;
     a.node_f4 = node_f4;
     a.qleaves = qn ? c->qleaves.p : nullptr;
+    a.n_qnodes = qn ? c->q_stride / zrt::kQuantNodeF4 : 0u;
+    a.n_qleaves = qn ? c->n_qleaves : 0u;
     a.lds_rows = lds_rows;
     if (stack_depth > lds_rows) {
       const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
@@ -5397,6 +5411,8 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.wide_stride = qn ? c->q_stride : c->wide_stride;
     a.node_f4 = node_f4;
     a.qleaves = qn ? c->qleaves.p : nullptr;
+    a.n_qnodes = qn ? c->q_stride / zrt::kQuantNodeF4 : 0u;
+    a.n_qleaves = qn ? c->n_qleaves : 0u;
     a.error_flag = reinterpret_cast<uint32_t*>(c->scratch.p + zrt::kErrorSlot);
     a.n_list = c->use_bvh ? 0 : c->n_prims;
     a.tri_rcp_fast = c->tri_rcp_fast;
@@ -5518,6 +5534,80 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
       }
     }
     (void)where;
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_debug_qnodes(const zrt_scene* scene, uint64_t* n_checked) {
+  if (!n_checked) return fail(ZRT_E_INVALID, "null argument");
+  *n_checked = 0;
+  int rc = zrt::validate_scene(scene);
+  if (rc) return rc;
+  if (scene->n_prims <= 10) return fail(ZRT_E_INVALID, "no BVH for <= 10 surfaces (raytrace.zig:124-133)");
+  try {
+    const char* prev = std::getenv("ZRT_QNODES");
+    const std::string saved = prev ? prev : "";
+    setenv("ZRT_QNODES", "1", 1);
+    zrt::HostScene h;
+    zrt::flatten_scene(&h, scene, true, -1);
+    if (prev) setenv("ZRT_QNODES", saved.c_str(), 1);
+    else unsetenv("ZRT_QNODES");
+    if (!h.q_ok) return fail(ZRT_E_UNSUPPORTED, "the encoder refused this tree (a non-finite plane)");
+    const uint32_t nn = h.q_stride / zrt::kQuantNodeF4, nw = h.wide_stride / 8u;
+    if (nn != nw) return fail(ZRT_E_UNSUPPORTED, "compressed and full trees differ in node count");
+    auto bad = [](const std::string& what, uint32_t o, uint32_t i, int k) {
+      return fail(ZRT_E_UNSUPPORTED, what + " (octant " + std::to_string(o) + ", node " + std::to_string(i) + ", slot " +
+                                         std::to_string(k) + ")");
+    };
+    for (uint32_t o = 0; o < 8; ++o) {
+      for (uint32_t i = 0; i < nn; ++i) {
+        const float4* F = &h.wn[size_t(o) * h.wide_stride + 8u * i];  // full node, this octant's copy
+        uint32_t W[16];
+        std::memcpy(W, &h.qn[size_t(o) * h.q_stride + zrt::kQuantNodeF4 * i], sizeof(W));
+        float org[3], step[3];
+        std::memcpy(org, W, 12);
+        for (int a = 0; a < 3; ++a) step[a] = std::ldexp(1.0f, int((W[3] >> (8 * a)) & 0xffu) - 127);
+        int32_t fr[4], qr[4], fb[4];
+        std::memcpy(fr, &F[6], 16);
+        std::memcpy(fb, &F[7], 16);
+        std::memcpy(qr, &W[10], 16);
+        for (int k = 0; k < 4; ++k) {
+          const float* fn = reinterpret_cast<const float*>(F);
+          const bool empty = qr[k] == zrt::kEmptyRef;
+          for (int a = 0; a < 3 && !empty; ++a) {
+            const double qn = double((W[4 + a] >> (8 * k)) & 0xffu), qf = double((W[7 + a] >> (8 * k)) & 0xffu);
+            const double dn = double(org[a]) + qn * double(step[a]), df = double(org[a]) + qf * double(step[a]);
+            if (double(float(dn)) != dn || double(float(df)) != df) return bad("a plane does not decode exactly", o, i, k);
+            const bool neg = (o >> a) & 1u;  // the near plane is the max one
+            const double full_n = fn[4 * a + k], full_f = fn[4 * (3 + a) + k];
+            if (neg ? !(dn >= full_n && df <= full_f) : !(dn <= full_n && df >= full_f))
+              return bad("a decoded box does not contain the full node's", o, i, k);
+          }
+          if (!empty && qr[k] >= 0 && qr[k] != fr[k]) return bad("an inner child ref differs", o, i, k);
+          if (!empty && qr[k] < 0) {
+            const bool sph = qr[k] < -zrt::kSphereSlotBias;
+            const uint32_t L = uint32_t(-(sph ? qr[k] + zrt::kSphereSlotBias : qr[k]) - 1);
+            if (size_t(L) * zrt::kLeafRecF4 + 1 >= h.ql.size()) return bad("a leaf record index past the records", o, i, k);
+            const float4 mn = h.ql[zrt::kLeafRecF4 * size_t(L)], mx = h.ql[zrt::kLeafRecF4 * size_t(L) + 1];
+            const float m[3] = {mn.x, mn.y, mn.z}, M[3] = {mx.x, mx.y, mx.z};
+            for (int a = 0; a < 3; ++a) {
+              const bool neg = (o >> a) & 1u;
+              const float full_n = fn[4 * a + k], full_f = fn[4 * (3 + a) + k];
+              const float rn = neg ? M[a] : m[a], rf = neg ? m[a] : M[a];
+              if (std::memcmp(&rn, &full_n, 4) || std::memcmp(&rf, &full_f, 4)) return bad("a leaf record's box differs", o, i, k);
+            }
+            int32_t ra, rb;
+            std::memcpy(&ra, &mn.w, 4);
+            std::memcpy(&rb, &mx.w, 4);
+            const int32_t full_a = sph ? fr[k] + zrt::kSphereSlotBias : fr[k];
+            if (ra != full_a || rb != fb[k] || sph != (fr[k] < -zrt::kSphereSlotBias))
+              return bad("a leaf record's refs differ", o, i, k);
+          }
+          ++*n_checked;
+        }
+      }
+    }
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
