@@ -1,12 +1,12 @@
 """Compressed wide nodes (accel_build.hpp quantize_wide, render.hip wide_iter_q;
 DESIGN.md §3 "Compressed nodes") against the oracle.
 
-The default uses them for trees of >= 65536 wide nodes (the C5 mesh, covered by
-test_gpu_parity.py's scene-6 tests); ZRT_QNODES=1 forces them on the small
-scenes here, so every adversarial ray set of the full-node traversal runs
-through the 64-B nodes and their leaf records too: zrt_trace (FAST) and the
-path-pool render (MODE 8, and MODE 9 with the grazing-triangle guard) must give
-the oracle's answers bit for bit.
+They are opt-in (ZRT_QNODES=1: measured slower than the full nodes on the C5
+mesh); the tests force them on every BVH scene and on the C5 mesh,
+so every adversarial ray set of the full-node traversal runs through the 64-B
+nodes and their leaf records too: zrt_trace (FAST) and the path-pool render
+(MODE 8, and MODE 9 with the grazing-triangle guard) must give the oracle's
+answers bit for bit.
 
 Run on an MI355X: ``pytest -m gpu``.
 """
@@ -148,3 +148,40 @@ def test_qnodes_frame_equals_full_nodes(scenes, monkeypatch):
     P.assert_bit_exact(comp, full)
     for k in P.COUNTERS:
         assert cs[k] == fs[k], k
+
+
+@pytest.mark.parametrize("rows", [None, "2"])
+def test_qnodes_c5_substitute_depth20_vs_golden(scenes, rows, qnodes, monkeypatch):
+    """Scene 6 (the 1.6 M-triangle C5 mesh, its tree past the 16-bit stack) on the
+    compressed nodes: 32x32 x 2 spp at depth 20 against the oracle's golden frame,
+    counters and per-scanline counters (tests/golden/c5_depth20.npz); rows="2"
+    forces the stack onto its global rows past 2 LDS rows.  STATS reports 64-B nodes."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_depth20.npz"))
+    w, h, spp, depth, chunk = (int(x) for x in g["params"])
+    monkeypatch.setenv("ZRT_ATT_LDS_ROWS", "0")
+    if rows:
+        monkeypatch.setenv("ZRT_STACK_LDS_ROWS", rows)
+    s = scenes(6)
+    p = z.RenderParams(w, h, spp, depth, sample_chunk=chunk)
+    gpu, gs, grows = z.render_progress(s, s.camera, p)
+    P.assert_bit_exact(gpu, g["image"])
+    for name, v in zip(g["counter_names"], g["counters"]):
+        assert gs[str(name)] == int(v), name
+    np.testing.assert_array_equal(grows, g["rows"])
+    _, st = z.render(s, s.camera, z.RenderParams(16, 16, 1, depth, flags=z.ZRT_FLAG_STATS))
+    assert st["node_bytes"] == 64
+
+
+def test_qnodes_c5_grazing_triangles(scenes, qnodes):
+    """The grazing-triangle set on scene 6 through the compressed nodes: equal to
+    the REFERENCE traversal (which reads the reference BVH, not the wide tree)."""
+    import grazing_tris as G
+    s = scenes(6)
+    pr = P.prim_array(s.view.contents)
+    mins, maxs, left, right, _ = z.bvh_build_device(s)
+    o, d = G.grazing_triangle_rays(pr, mins, maxs, left, right, n=4000, seed=2, span=G.scene_span(pr))
+    t_ref, p_ref = z.trace(s, z.RenderParams(1, 1, 1, 1, traversal=z.ZRT_TRAVERSAL_REFERENCE), o, d)
+    t, p = z.trace(s, FAST, o, d)
+    assert (p_ref >= 0).mean() > 0.5
+    P.assert_same_hits(t, p, t_ref, p_ref)

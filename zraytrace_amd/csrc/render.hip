@@ -4187,12 +4187,15 @@ bool use_pool(const zrt_ctx* c, bool stk16) {
   (void)c;
   return !stk16;
 }
-// Compressed wide nodes (wide_iter_q, MODE 8 / 9) for this tree?  ZRT_QNODES=0/1
-// forces it; default: trees of the path-pool loop's size (>= 65536 wide nodes,
-// past the 16-bit stack), whose octant copies outgrow the caches.
+// Compressed wide nodes (wide_iter_q, MODE 8 / 9) for this tree?  ZRT_QNODES=1
+// builds them (for trees of the path-pool loop's size, >= 65536 wide nodes, past the
+// 16-bit stack, or any tree when forced); off by default: on the C5 mesh the pool
+// over compressed nodes ran 7.17 Gray/s against 8.57 over the full nodes - each
+// opened leaf's record is one more dependent fetch (DESIGN.md §3 "Compressed nodes")
 bool want_qnodes(uint32_t n_wide) {
   if (const char* e = std::getenv("ZRT_QNODES")) return std::atoi(e) != 0;
-  return n_wide >= 65536;
+  (void)n_wide;
+  return false;
 }
 // Top levels of a compressed tree served from LDS (ZRT_QTOP overrides): every ray
 // reads the root and a level-1 node, most a level-2 node - with 64-B nodes the
