@@ -378,3 +378,24 @@ def test_distant_camera_triangle_scene_does_not_replay(scenes):
     assert same_bits(img, ref)
     assert st["rays_processed"] == rs["rays_processed"]
     assert st["order_replays"] <= 0.01 * st["rays_processed"], st["order_replays"]
+
+
+@pytest.mark.parametrize("loop", ["wavefront", "pool"])
+def test_scheduled_launch_of_other_loops(scenes, loop, monkeypatch):
+    """The scheduling probe (a lockstep launch with its own LDS plan, spp >= 128)
+    in front of a wavefront / path-pool render on a frame large enough that the
+    probe's grid equals the render's (> 4096 tiles): the probe's global
+    attenuation and stack rows fit the buffers it shares with the render launch
+    (round 5: the wavefront render's 12 LDS rows left the probe's rows 2x too few),
+    and the frame equals the lockstep loop's bit for bit."""
+    s = scenes(3)
+    p = z.RenderParams(640, 640, 128, 20)
+    monkeypatch.setenv("ZRT_WF", "0")
+    monkeypatch.setenv("ZRT_POOL", "0")
+    ref, rs = z.render(s, s.camera, p)
+    monkeypatch.setenv("ZRT_WF", "1" if loop == "wavefront" else "0")
+    monkeypatch.setenv("ZRT_POOL", "1" if loop == "pool" else "0")
+    img, st = z.render(s, s.camera, p)
+    assert same_bits(img, ref)
+    for k in COUNTERS:
+        assert st[k] == rs[k], k

@@ -4432,8 +4432,17 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
     }
     a.stack_ovf = pa.stack_ovf = c->stack_ovf.p;
   }
-  // the global attenuation rows: the render launch's buffer holds the probe's rows
-  // (fewer lanes, at least as many LDS rows: zrt_ctx_render_tiles sizes it)
+  // its global attenuation rows, [row][lane] past its LDS rows: the render launch's
+  // buffer, grown if the probe's plan keeps fewer rows in LDS than the render's (the
+  // wavefront loop keeps 12, the lockstep probe 4)
+  {
+    const uint64_t need = std::max<uint64_t>(1, a.max_depth - std::min(a.max_depth, pp.att_rows)) * pa.n_lanes;
+    if (c->att.n < need) {
+      HIPCHK(hipStreamSynchronize(st));  // (the previous launch may still read the old buffer)
+      c->att.alloc(need);
+    }
+    a.att = pa.att = c->att.p;
+  }
   HIPCHK(hipMemsetAsync(c->probe_scratch.p, 0, kScratchSlots * sizeof(unsigned long long), st));
   void* fn = prng == ZRT_PRNG_XOSHIRO256 ? probe_ptr<ZRT_PRNG_XOSHIRO256>(stk16)
                                          : probe_ptr<ZRT_PRNG_XOROSHIRO128>(stk16);
