@@ -60,6 +60,16 @@ def test_device_math_bit_exact():
     ys[:4] = [0, -0.0, 1, 0]
     xs[:4] = [-1, -1, 0, 1]
     assert same_bits(z.debug_math(5, ys, xs), O.math2("atan2", ys, xs)).all(), "atan2"
+    # magnitudes over the whole exponent range: the short divisions inside atan / atan2
+    # (dev::div_rn) fall back to IEEE `/` where an operand or quotient leaves [2^-50, 2^50]
+    mag = lambda k: (rng.choice([-1, 1], k) * 10.0 ** rng.uniform(-40, 38, k)).astype(np.float32)
+    ys, xs = mag(n), mag(n)
+    assert same_bits(z.debug_math(5, ys, xs), O.math2("atan2", ys, xs)).all(), "atan2 wide"
+    aw = mag(n)
+    assert same_bits(z.debug_math(3, aw), O.math1("atan", aw)).all(), "atan wide"
+    cw = np.concatenate([(rng.choice([-1, 1], n) * 10.0 ** rng.uniform(-45, 0, n)).astype(np.float32),
+                         np.nextafter(np.float32([1, -1]), np.float32(0))])
+    assert same_bits(z.debug_math(2, cw), O.math1("acos", cw)).all(), "acos wide"
     p = np.concatenate([rng.random(n, dtype=np.float32), np.array([0, 1, 2, 1e-7, 2 ** -24], np.float32)])
     assert same_bits(z.debug_math(6, p), O.math2("pow", p, np.full_like(p, 5.0))).all(), "pow5"
     # IEEE correctly rounded sqrt and division (HIP's default for f32)
