@@ -399,3 +399,39 @@ def test_scheduled_launch_of_other_loops(scenes, loop, monkeypatch):
     assert same_bits(img, ref)
     for k in COUNTERS:
         assert st[k] == rs[k], k
+
+
+def _step_eff(s, p):
+    """Lane steps / (64 x loop trips that ran one) of a STATS launch (slots 22, 23)."""
+    import torch
+    ctx = z.RenderContext(s, p)
+    buf = torch.zeros(ctx.tile_count(p) * 64 * 3, dtype=torch.float32, device="cuda")
+    ctx.render_tiles(s.camera, z.RenderParams(**{**p.__dict__, "flags": z.ZRT_FLAG_STATS}), buf.data_ptr())
+    ctx.sync()
+    dc = ctx.debug_counters(32)
+    ctx.close()
+    return dc[23] / (64.0 * dc[22])
+
+
+@pytest.mark.parametrize("idx,free", [(3, True), (2, False)])
+def test_auto_sync_from_probe(scenes, idx, free, monkeypatch):
+    """The lockstep interval the render launch takes from the scheduling probe
+    (render.hip auto_sync): the teapot (C3's scene), whose waves mostly wait for their
+    longest path, runs its lanes free through the unit - more lanes step per loop
+    trip - and the bunny (C4's) keeps them in step; either way the frame and the
+    counters are the fixed interval's, bit for bit."""
+    s = scenes(idx)
+    p = z.RenderParams(128, 128, 128, 20)
+    monkeypatch.setenv("ZRT_AUTO_SYNC", "0")
+    ref, rs = z.render(s, s.camera, p)
+    fixed = _step_eff(s, p)
+    monkeypatch.delenv("ZRT_AUTO_SYNC")
+    img, st = z.render(s, s.camera, p)
+    auto = _step_eff(s, p)
+    assert same_bits(img, ref)
+    for k in COUNTERS:
+        assert st[k] == rs[k], k
+    if free:
+        assert auto > fixed + 0.05, (auto, fixed)
+    else:
+        assert auto == fixed, (auto, fixed)
