@@ -33,7 +33,10 @@ def _ensure_built():
     csrc = os.path.join(REPO, "zraytrace_amd", "csrc")
     from zraytrace_amd import build_id_of_sources
     want = build_id_of_sources()
-    if not os.path.exists(lib) or _lib_source_id(lib) != want:
+    # (ZRT_LIB: the tests run an A/B build variant; the in-tree library is left as
+    # it is - rebuilding it from the tree's sources here would make a later A/B
+    # run of "the shipped library" in the same session the variant too)
+    if not os.environ.get("ZRT_LIB") and (not os.path.exists(lib) or _lib_source_id(lib) != want):
         # missing, or stale against its sources: rebuild, and
         # refuse to test a library that still does not match the tree
         subprocess.run(["make", "-s", "-j8", "-C", csrc], check=True)

@@ -12,6 +12,18 @@ for r in $(seq 1 $ROUNDS); do
     v=${spec%%@*}; EXTRA_ARGS=(); [ "$spec" != "$v" ] && EXTRA_ARGS=(--chunk ${spec#*@})
     if [ "$v" == "default" ]; then LIB=$R/zraytrace_amd/libzrt.so; else LIB=$R/abvar/$v/libzrt.so; fi
     ZRT_LIB=$LIB timeout -k 10 300 python $R/bench.py --no-cpu-baseline "$@" "${EXTRA_ARGS[@]}" > $OUT/$spec.$r.json 2> $OUT/$spec.$r.err || { echo "variant $v failed"; tail -5 $OUT/$spec.$r.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('$OUT/$spec.$r.json')); print('$spec', $r, d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['roofline']['algorithmic']['per_ray'])"
+    python -c "import json,sys; d=json.load(open('$OUT/$spec.$r.json')); print('$spec', $r, d['build_id'], d['value'], 'Mrays/s', d['kernel_ms_avg'], 'ms', d['roofline']['algorithmic']['per_ray'])"
   done
 done
+# every variant must have run its own library (a library rebuilt in place between
+# builds - tests/conftest.py rebuilds a stale in-tree one - would make two the same)
+python - "$OUT" <<'PYEOF' || exit 1
+import glob, json, os, sys
+ids = {}
+for f in glob.glob(os.path.join(sys.argv[1], "*.json")):
+    v = os.path.basename(f).rsplit(".", 2)[0].split("@")[0]  # (v@chunk: one library, several chunks)
+    ids.setdefault(json.load(open(f))["build_id"], set()).add(v)
+dup = [sorted(vs) for vs in ids.values() if len(vs) > 1]
+if dup:
+    sys.exit(f"A/B invalid: variants {dup} ran the same library")
+PYEOF

@@ -153,7 +153,7 @@ __device__ __forceinline__ void sincos_z(float xin, float* s_out, float* c_out) 
 __device__ __forceinline__ float acos_r32(float z) {
   const float p = z * (1.6666586697e-01f + z * (-4.2743422091e-02f + z * -8.6563630030e-03f));
   const float q = 1.0f + z * -7.0662963390e-01f;
-  return div_rn(p, q);
+  return p / q;
 }
 __device__ __forceinline__ float acos_z(float x) {
   const float pio2_hi = 1.5707962513e+00f;
@@ -177,7 +177,7 @@ __device__ __forceinline__ float acos_z(float x) {
   const float z = (1.0f - x) * 0.5f;
   const float s = sqrt_rn(z);
   const float df = __uint_as_float(__float_as_uint(s) & 0xfffff000u);
-  const float c = div_rn(z - df * df, s + df);
+  const float c = (z - df * df) / (s + df);
   const float w = acos_r32(z) * s + c;
   return 2.0f * (df + w);
 }
@@ -202,18 +202,18 @@ __device__ __forceinline__ float atan_z(float xin) {
     if (ix < 0x3f980000u) {
       if (ix < 0x3f300000u) {
         id = 0;
-        x = div_rn(2.0f * x - 1.0f, 2.0f + x);
+        x = (2.0f * x - 1.0f) / (2.0f + x);
       } else {
         id = 1;
-        x = div_rn(x - 1.0f, x + 1.0f);
+        x = (x - 1.0f) / (x + 1.0f);
       }
     } else {
       if (ix < 0x401c0000u) {
         id = 2;
-        x = div_rn(x - 1.5f, 1.0f + 1.5f * x);
+        x = (x - 1.5f) / (1.0f + 1.5f * x);
       } else {
         id = 3;
-        x = div_rn(-1.0f, x);
+        x = -1.0f / x;
       }
     }
   }
@@ -265,7 +265,7 @@ __device__ __forceinline__ float atan2_z(float y, float x) {
   if (ix + (26u << 23) < iy || iy == 0x7f800000u) return (m & 1) ? -pi / 2.0f : pi / 2.0f;
   float z;
   if ((m & 2) && iy + (26u << 23) < ix) z = 0.0f;
-  else z = atan_z(__builtin_fabsf(div_rn(y, x)));
+  else z = atan_z(__builtin_fabsf(y / x));
   switch (m) {
     case 0: return z;
     case 1: return -z;
