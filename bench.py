@@ -113,7 +113,86 @@ def ubench_peaks():
     return p, src + "; VALU issue: MI355X_MICROARCH.md, 0.5 wave64 inst/SIMD/clk"
 
 
-def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None):
+# zrt_ctx_debug_counters slots of the STATS launch (render.hip kVNodeTrips ..):
+# the FAST loops' vector-memory wave-instructions by shape
+DC_SHAPES = {"vnode_trips": 32, "vnode_lines": 33, "snode_trips": 34, "rb_trips": 35, "vprim_trips": 36,
+             "vprim_lines": 37, "sprim_trips": 38, "vshade_trips": 39, "att_w_trips": 40, "att_r_trips": 41,
+             "vnode_cost": 42, "vprim_cost": 43}
+
+
+def shape_costs():
+    """TD (vector data return) busy cycles per wave-instruction of each load shape
+    the render kernel issues, measured alone with the whole chip by
+    tools/ubench_shapes.hip under rocprofv3 (profiles/ubench.json "shapes"): a
+    wave64 dwordx4 load costs 16 cycles (1 KiB of lane data at 64 B/clk) whether
+    its 64 lanes read 1, 2 or 4 records, one cycle per distinct 64-B line beyond
+    16 (64 for 64 lines); a dword per lane (256 B, the scratch layout) costs ~5.7
+    as a load and ~10.7 as a store.  None if the file has no shapes."""
+    try:
+        with open(os.path.join(REPO, "profiles", "ubench.json")) as f:
+            sh = json.load(f)["shapes"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+    def td(case):
+        return sh[case]["per_vmem_inst"]["td_busy_cycles_per_cu"]
+    return {"x4": td("node_k1_l2"), "x4_k64": td("node_k64_l2"), "dword_load": td("lane_dwords_load"),
+            "dword_store": td("lane_dwords_store"), "prim_x4": td("prim_k1"),
+            "flat_lds_x4": td("node_lds_flat_k1") if "node_lds_flat_k1" in sh else None,
+            "source": "profiles/ubench.json shapes (tools/ubench_shapes.hip, rocprofv3 --pmc)"}
+
+
+def data_return_model(pmc, dc, n_units, kernel_s, clk):
+    """The render launch's vector-memory data-return cycles, modelled (DESIGN.md §4
+    "The data-return model"): the STATS launch's wave-instruction counts per shape
+    (dc: zrt_ctx_debug_counters) x each shape's calibrated cost (shape_costs), plus
+    the vector-memory instructions PMC counts beyond those (scratch: spilled-register
+    reloads and stores, one dword per lane) at the dword costs.  frac = modelled
+    cycles per CU / the launch's cycles: the share of the data-return path's
+    calibrated throughput the launch needs.  Also returned: the model / TD_TD_BUSY
+    ratio (1: the TD busy counter measures throughput; TD_TC_STALL: the part of it
+    spent waiting for the cache)."""
+    c = shape_costs()
+    sq, cache = (pmc or {}).get("sq") or {}, (pmc or {}).get("cache") or {}
+    if not c or not sq.get("SQ_INSTS_VMEM_RD") or dc is None or len(dc) <= max(DC_SHAPES.values()):
+        return None
+    n = {k: int(dc[i]) for k, i in DC_SHAPES.items()}
+    if not n["vnode_trips"] and not n["snode_trips"]:
+        return None  # not a FAST loop
+    x4 = c["x4"]
+    per_line = (c["x4_k64"] - x4) / 48.0  # cycles per distinct line past 16
+    rd_known = 7 * n["vnode_trips"] + n["rb_trips"] + 3 * n["vprim_trips"] + n["vshade_trips"] + n["att_r_trips"]
+    wr_known = n["att_w_trips"] + n_units
+    scratch_rd = max(0.0, sq["SQ_INSTS_VMEM_RD"] - rd_known)
+    scratch_wr = max(0.0, sq.get("SQ_INSTS_VMEM_WR", 0.0) - wr_known)
+    parts = {
+        # 7 dwordx4 per node trip (the 8th, the leaf refs, under rb), max(16, distinct) lines each
+        "node_loads": 7 * (x4 * n["vnode_trips"] + per_line * (n["vnode_cost"] - 16 * n["vnode_trips"])),
+        "leaf_refs": x4 * n["rb_trips"],
+        "prim_loads": 3 * (c["prim_x4"] * n["vprim_trips"] + per_line * (n["vprim_cost"] - 16 * n["vprim_trips"])),
+        "shade_loads": x4 * n["vshade_trips"],
+        "att_rows": c["dword_store"] * n["att_w_trips"] + c["dword_load"] * n["att_r_trips"],
+        "chunk_sums": 4 * c["dword_store"] * n_units,  # one 1 KiB store per unit = 4 x 256 B
+        "scratch_loads": c["dword_load"] * scratch_rd,
+        "scratch_stores": c["dword_store"] * scratch_wr,
+    }
+    total = sum(parts.values())
+    cyc = kernel_s * clk  # the launch's cycles per CU
+    out = {"bound": "vmem_data_return", "cycles_per_launch": float(f"{total:.4e}"),
+           "frac": round(total / N_CU / cyc, 4),
+           "parts_frac": {k: round(v / N_CU / cyc, 4) for k, v in parts.items()},
+           "inputs": {**n, "n_units": int(n_units), "pmc_vmem_rd": sq["SQ_INSTS_VMEM_RD"],
+                      "pmc_vmem_wr": sq.get("SQ_INSTS_VMEM_WR"), "scratch_rd_insts": scratch_rd,
+                      "scratch_wr_insts": scratch_wr},
+           "costs_td_cycles_per_inst": c}
+    if cache.get("TD_TD_BUSY_sum"):
+        out["model_over_td_busy"] = round(total / cache["TD_TD_BUSY_sum"], 4)
+    if cache.get("TD_TC_STALL_sum") and cache.get("TD_TD_BUSY_sum"):
+        out["td_tc_stall_over_td_busy"] = round(cache["TD_TC_STALL_sum"] / cache["TD_TD_BUSY_sum"], 4)
+    return out
+
+
+def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None, model_in=None):
     """The render launch against every ceiling it could be bound by.  Per ceiling:
     the PMC count per launch (rocprofv3 pass of this exact config) / the launch's
     HIP-event time measured in this run = achieved, against the measured per-clock
@@ -123,7 +202,11 @@ def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None):
       l1_access   TCP (L1) cache accesses; peak = the best load pattern's rate
       l2_lines    L1 -> L2 read requests; peak = an all-miss L1 pattern's rate
       hbm         (2 FETCH_SIZE + WRITE_SIZE) KiB; peak = 8 TB/s
-    bound = the ceiling with the largest fraction."""
+      vmem_model  modelled data-return cycles per CU (data_return_model: the STATS
+                  launch's wave-instructions per load shape x their ubench_shapes
+                  costs); peak = every cycle of the launch
+    bound = the rate ceiling with the largest fraction; the TD busy
+    counter is reported beside the model, not chosen, when the model exists."""
     out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
            "kernel_s": round(kernel_s, 6)}
     if not pmc:
@@ -156,8 +239,20 @@ def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None):
         out["pmc_build_id"] = pmc.get("build_id")
         if cache.get("TCC_HIT_sum") is not None and cache.get("TCC_MISS_sum"):
             out["l2_hit_frac"] = round(cache["TCC_HIT_sum"] / (cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"]), 4)
+    if pmc and model_in is not None:
+        m = data_return_model(pmc, model_in[0], model_in[1], kernel_s, clk)
+        if m:
+            out["data_return_model"] = m
+            rows["vmem_model"] = {"per_launch": m["cycles_per_launch"],
+                                  "achieved": float(f"{m['cycles_per_launch'] / N_CU / kernel_s:.4e}"),
+                                  "peak": float(f"{clk:.4e}"), "unit": "modelled data-return cycles/s per CU",
+                                  "frac": m["frac"]}
     if rows:
-        b = max(rows, key=lambda k: rows[k]["frac"])
+        # TD_TD_BUSY counts cycles TD is processing OR waiting for data: a utilisation,
+        # not a rate (ubench_shapes: ~0.98 at every saturating shape), so where the
+        # data-return model exists the bound is chosen among the rates
+        cand = [k for k in rows if not (k == "vmem_td" and "vmem_model" in rows)]
+        b = max(cand, key=lambda k: rows[k]["frac"])
         out.update({"bound": b, "achieved": rows[b]["achieved"], "peak": rows[b]["peak"], "unit": rows[b]["unit"],
                     "frac": rows[b]["frac"]})
         if "valu_issue" in rows and out.get("valu_lane_util"):
@@ -363,9 +458,15 @@ def main_multi(args, devices):
         "frame_sha1_n1": ref_hash,
         "frame_equal_to_n1": (frame_sha1 == ref_hash) if ref_hash else None,
         "build_id": z.build_id(),
+        "abi_version": z.lib().zrt_abi_version(),
         "per_rank_ms": {"kernel": [round(x, 3) for x in per_rank],
                         "gather_assemble": round(sum(gather_ms) / len(gather_ms), 3)},
     }
+    if len(distinct) < n:
+        out["scaling_note"] = (f"{n} ranks share {len(distinct)} GPU(s): value rehearses the N-rank path (launches, "
+                               "gather, assemble, frame equality) and is not a scaling figure; the ranks' kernels "
+                               "run concurrently on the same CUs, so per_rank_ms.kernel is each rank's share of "
+                               "one GPU, not its time alone")
     print(json.dumps(out), flush=True)
 
 
@@ -491,12 +592,12 @@ def main():
             pe, why = None, "PMC passes are taken at N=1 only"
         if bid.split("-")[0] != z.build_id_of_sources():
             pe, why = None, f"libzrt.so ({bid}) is stale against its sources ({z.build_id_of_sources()})"
-        roof = roofline(pe, avg_kernel_s, algo, diag, why)
+        dc = fr.ctx.debug_counters(48)  # the STATS launch's counters (shapes, SIMD efficiency, writes)
+        roof = roofline(pe, avg_kernel_s, algo, diag, why, model_in=(dc, n_units))
         # what the render launch writes to memory: each work unit's
         # 64 chunk sums (float4), the attenuation rows past the LDS ones (float4; STATS
         # counter kAttWrites of the diagnostic launch) and, on deep trees, the traversal
         # stack entries past the LDS rows (u32; kStackOvfWrites)
-        dc = fr.ctx.debug_counters(32)
         wb = {"chunk_sums_B": 16 * 64 * n_units, "att_rows_B": 4 * int(dc[28]),  # 4-B att codes
               "stack_rows_B": 4 * int(dc[30])}  # FAST stack entries past the LDS rows (kStackOvfWrites)
         wb["payload_B"] = wb["chunk_sums_B"] + wb["att_rows_B"] + wb["stack_rows_B"]
@@ -581,6 +682,7 @@ def main():
             "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
             "frame_sha1": frame_sha1,
             "build_id": bid,
+            "abi_version": z.lib().zrt_abi_version(),
             "per_rank_ms": {"kernel": [round(x[0], 3) for x in per_rank],
                             "gather": [round(x[1], 3) if x[1] == x[1] else None for x in per_rank]},
         }

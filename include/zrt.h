@@ -502,6 +502,17 @@ int zrt_debug_division(uint64_t n, uint64_t* counts, uint32_t device);
  * share).  n_checked: the number of plans checked.  ZRT_E_UNSUPPORTED names the
  * first violation. */
 int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked);
+/* Host-side check of the global buffers the launches of a FAST frame share (no
+ * device needed): for every sampling loop, stack width, PRNG, node format, a
+ * range of max depths and grid sizes, zrt_render's sizing of the attenuation
+ * rows and stack overflow rows (the render launch's need, grown to its
+ * scheduling probe's) is checked against what each of the two launches needs
+ * (zrt::buffer_need; the same check guards every launch, ZRT_E_UNSUPPORTED
+ * instead of a device fault).  legacy = 1 applies the sizing before the round-5
+ * fix (the probe shared the render's attenuation rows without growing them):
+ * it must fail where a loop keeps more rows in LDS than the probe's 4.
+ * n_checked: configurations checked. */
+int zrt_debug_buffer_plans(const zrt_scene* scene, uint32_t legacy, uint32_t* n_checked);
 /* Host-side check of the compressed wide nodes built for this scene (no device
  * needed): every plane of every node's eight octant copies decodes exactly to
  * an f32, every slot's decoded box contains the full node's box of that slot,

@@ -324,8 +324,27 @@ def test_lds_plans_disjoint(scenes, index):
     rows, materials) disjoint, inside the plan and float4-aligned, and the lockstep
     plan inside its 6-block share (render.hip check_plan).  No device needed."""
     n = z.debug_lds_plans(scenes(index))
-    # modes 0-2 one loop each, mode 3 lockstep / wavefront / pool (full and compressed nodes); x stk16 x prng x depth
-    assert n == (1 + 1 + 1 + 1 + 1 + 2) * 2 * 2 * 6
+    # modes 0-2 one loop each, mode 3 lockstep / wavefront / pool (full nodes, and compressed
+    # ones where the scene has a tree: their real top levels); x stk16 x prng x depth
+    comp = 0 if index == 1 else 1
+    assert n == (1 + 1 + 1 + 1 + 1 + 1 + comp) * 2 * 2 * 6
+
+
+@pytest.mark.parametrize("index", [0, 2, 3, 4])
+def test_shared_buffer_sizing_covers_every_launch(scenes, index):
+    """the global rows a FAST frame's launches share - the
+    attenuation rows past the LDS ones and the stack rows past the LDS ones - are
+    sized (zrt_render, schedule_tiles) to cover the render launch AND its scheduling
+    probe, for every loop x stack width x PRNG x node format x depth x grid
+    (render.hip buffer_need / check_buffers, the same check that guards each launch).
+    The sizing before commit 4072f5f (the probe reused the render's attenuation rows
+    without growing them) must fail where the render keeps more LDS rows than the
+    probe's 4: the wavefront loop's 12 - the round-5 GPU fault of ZRT_WF=1 on C3."""
+    s = scenes(index)
+    n = z.debug_buffer_plans(s)
+    assert n >= 3 * 2 * 2 * 9 * 3  # lockstep, wavefront, pool (+ compressed) x stk16 x prng x depth x grid
+    with pytest.raises(z.ZrtError, match="scheduling probe: needs .* attenuation-row entries.*loop 1"):
+        z.debug_buffer_plans(s, legacy=True)
 
 
 @pytest.mark.parametrize("index", [0, 2, 3, 4])

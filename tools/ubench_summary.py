@@ -31,6 +31,79 @@ def case_of(name, k):
     return base, k
 
 
+def shapes_summary(d):
+    """tools/ubench_shapes.hip under rocprofv3 --pmc (passes sh1..shN): every case is
+    its own kernel, launched 6 times in the order of events_shapes.json (the first a
+    warm-up).  Per case: the PMC counts per timed dispatch, and per vector-memory
+    wave-instruction: TD and TA busy cycles (per CU), TCP accesses, L1 -> L2 requests;
+    with the HIP-event time: CU cycles per instruction at the clock the pass saw."""
+    ev_path = os.path.join(d, "events_shapes.json")
+    if not os.path.exists(ev_path):
+        return None
+    with open(ev_path) as f:
+        ev = json.load(f)
+    names = list(ev["shapes"].keys())
+    per = {}
+    for csvp in sorted(glob.glob(os.path.join(d, "sh*", "run_counter_collection.csv"))):
+        with open(csvp) as f:
+            rs = list(csv.DictReader(f))
+        # (the runtime's own kernels - hipMemset's fill - are not cases)
+        rs = [r for r in rs if not r["Kernel_Name"].lstrip().startswith("__amd")]
+        first = {}
+        for r in rs:
+            k, i = r["Kernel_Name"].split("(")[0], int(r["Dispatch_Id"])
+            first[k] = min(first.get(k, i), i)
+        kernels = sorted(first, key=first.get)
+        disp = {}
+        for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
+            k = r["Kernel_Name"].split("(")[0]
+            disp.setdefault(k, [])
+            if int(r["Dispatch_Id"]) not in disp[k]:
+                disp[k].append(int(r["Dispatch_Id"]))
+        for r in rs:
+            k = r["Kernel_Name"].split("(")[0]
+            if k not in kernels or kernels.index(k) >= len(names):
+                continue
+            if disp[k].index(int(r["Dispatch_Id"])) == 0:
+                continue  # warm-up
+            case = names[kernels.index(k)]
+            c = per.setdefault(case, {})
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+            c.setdefault(r["Counter_Name"], []).append((float(r["Counter_Value"]), dur))
+    out = {}
+    for case in names:
+        e = dict(ev["shapes"][case])
+        c = per.get(case, {})
+        avg = {k: sum(v for v, _ in xs) / len(xs) for k, xs in c.items()}
+        durs = [t for xs in c.values() for _, t in xs]
+        row = {"events": e, "pmc_per_dispatch": {k: float(f"{v:.4e}") for k, v in sorted(avg.items())}}
+        insts = avg.get("SQ_INSTS_VMEM_RD", 0.0) + avg.get("SQ_INSTS_VMEM_WR", 0.0)
+        row["inst_kind"] = "vmem"
+        if not insts and avg.get("SQ_INSTS_LDS"):
+            insts, row["inst_kind"] = avg["SQ_INSTS_LDS"], "lds"
+        if insts:
+            per_inst = {}
+            for k, lab in (("TD_TD_BUSY_sum", "td_busy_cycles_per_cu"), ("TA_TA_BUSY_sum", "ta_busy_cycles_per_cu"),
+                           ("TD_TC_STALL_sum", "td_tc_stall_cycles_per_cu"),
+                           ("TCP_TOTAL_CACHE_ACCESSES_sum", "tcp_accesses"),
+                           ("TCP_TCC_READ_REQ_sum", "l2_read_reqs")):
+                if k in avg:
+                    # TD / TA busy summed over the CUs that ran the instructions: per CU and
+                    # per instruction = sum / instructions (each instruction runs on one CU)
+                    per_inst[lab] = round(avg[k] / insts, 3)
+            row["per_vmem_inst"] = per_inst
+            if avg.get("GRBM_GUI_ACTIVE") and durs:
+                dur = sum(durs) / len(durs)
+                clk = avg["GRBM_GUI_ACTIVE"] / N_XCD / dur
+                row["clock_hz"] = float(f"{clk:.4e}")
+                # CU cycles per instruction at saturation: the launch's cycles x CUs / instructions
+                row["cu_cycles_per_inst"] = round(e["ms"] * 1e-3 * clk * ev["cus"] / insts, 3)
+                if avg.get("TD_TD_BUSY_sum"):
+                    row["td_busy_frac"] = round(avg["TD_TD_BUSY_sum"] / N_CU / (e["ms"] * 1e-3 * clk), 4)
+        out[case] = row
+    return out
+
+
 def main():
     d = sys.argv[1]
     best = {}
@@ -75,7 +148,10 @@ def main():
     }
     with open(os.path.join(d, "events.json")) as f:
         out["events"] = json.load(f)
-    out["source"] = "tools/ubench.hip under rocprofv3 --pmc (tools/gpu_ubench.sh)"
+    sh = shapes_summary(d)
+    if sh:
+        out["shapes"] = sh
+    out["source"] = "tools/ubench.hip, tools/ubench_shapes.hip under rocprofv3 --pmc (tools/gpu_ubench.sh)"
     print(json.dumps(out, indent=1))
 
 

@@ -309,7 +309,7 @@ class RenderContext:
         check(lib().zrt_ctx_stats(self._h, C.byref(st)))
         return st.as_dict()
 
-    def debug_counters(self, n: int = 32):
+    def debug_counters(self, n: int = 48):
         out = (C.c_uint64 * n)()
         check(lib().zrt_ctx_debug_counters(self._h, out, n))
         return list(out)
@@ -437,6 +437,19 @@ def debug_lds_plans(scene) -> int:
     view = scene.view if isinstance(scene, LoadedScene) else scene
     n = C.c_uint32()
     check(lib().zrt_debug_lds_plans(view, C.byref(n)))
+    return n.value
+
+
+def debug_buffer_plans(scene, legacy: bool = False) -> int:
+    """Host-side check of the global attenuation / stack-overflow rows a FAST frame's
+    launches share (zrt_debug_buffer_plans; no device): zrt_render's sizing against
+    the need of the render launch and of its scheduling probe, for every loop, stack
+    width, PRNG, node format and a range of depths and grids.  Returns the number of
+    configurations checked, raises ZrtError naming the first launch whose rows would
+    lie past its buffer.  legacy=True applies the sizing before the round-5 fix."""
+    view = scene.view if isinstance(scene, LoadedScene) else scene
+    n = C.c_uint32()
+    check(lib().zrt_debug_buffer_plans(view, 1 if legacy else 0, C.byref(n)))
     return n.value
 
 

@@ -178,6 +178,7 @@ SIGNATURES = [
                                 C.c_uint32, C.c_uint32]),
     ("zrt_debug_division", C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32]),
     ("zrt_debug_lds_plans", C.c_int, [C.POINTER(Scene), C.POINTER(C.c_uint32)]),
+    ("zrt_debug_buffer_plans", C.c_int, [C.POINTER(Scene), C.c_uint32, C.POINTER(C.c_uint32)]),
     ("zrt_debug_qnodes", C.c_int, [C.POINTER(Scene), C.POINTER(C.c_uint64)]),
 ]
 
@@ -213,15 +214,20 @@ def load(path: str = LIB_PATH):
     rebuild = "rebuild it (python -c 'import __graft_entry__ as g; g.build()')"
     # the ABI version first (every version exports zrt_abi_version): the struct
     # layouts below are this version's, so another version is refused before any
-    # symbol is bound (an A/B variant under ZRT_LIB is warned about, not refused)
+    # symbol is bound - an A/B variant under ZRT_LIB too (its Params / Stats would be
+    # read with this version's layouts), unless ZRT_ALLOW_ABI_MISMATCH=1 asks for it
     lib.zrt_abi_version.restype = C.c_int
     lib.zrt_abi_version.argtypes = []
     abi = lib.zrt_abi_version()
     if abi != ABI_VERSION:
         if in_tree:
             raise ImportError(f"{path} has ABI version {abi}, this binding expects {ABI_VERSION}: {rebuild}")
+        if os.environ.get("ZRT_ALLOW_ABI_MISMATCH") != "1":
+            raise ImportError(f"ZRT_LIB {path} has ABI version {abi}, this binding expects {ABI_VERSION} "
+                              "(set ZRT_ALLOW_ABI_MISMATCH=1 to bind it anyway)")
         import warnings
-        warnings.warn(f"ZRT_LIB {path} has ABI version {abi}, this binding expects {ABI_VERSION}")
+        warnings.warn(f"ZRT_LIB {path} has ABI version {abi}, this binding expects {ABI_VERSION} "
+                      "(bound anyway: ZRT_ALLOW_ABI_MISMATCH=1)")
     for name, restype, argtypes in SIGNATURES:
         if not hasattr(lib, name):
             if in_tree:

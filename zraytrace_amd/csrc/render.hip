@@ -132,16 +132,34 @@ struct KArgs {
   float graze_m;           // the grazing margins' coefficient (RayT::gm; DESIGN.md §3 "Grazing rays")
   float graze_leaf;        // ... of leaf slots' relative margin (RayT::gl, >= graze_m)
   float guard;             // the grazing-triangle guard (RayT::gk, wide_iter; 0: off)
+  uint64_t att_cap, ovf_cap;  // elements of `att` and of `stack_ovf` (StackT): row_ok's bounds
 };
+
 
 // error_flag bits (zrt_ctx_sync / zrt_ctx_stats / zrt_render report them as ZRT_E_UNSUPPORTED)
 constexpr uint32_t kErrOverflow = 1u;  // a traversal stack deeper than it was sized for
 constexpr uint32_t kErrLayout = 2u;    // the wide tree's encoding is not the one this kernel decodes
+constexpr uint32_t kErrBounds = 4u;    // STATS flavour: a global row index past its buffer (row_ok)
+
+// The STATS flavour's bounds check of a global row index (attenuation rows,
+// stack overflow rows) against its buffer (KArgs::att_cap / ovf_cap, set from the
+// allocations): past it, kErrBounds is raised and the access skipped, so a
+// sizing mistake the host check (zrt::check_buffers) missed reports instead of
+// faulting.  The timed flavour compiles it away.
+#ifndef ZRT_DEBUG_BOUNDS
+#define ZRT_DEBUG_BOUNDS 1
+#endif
+template <bool STATS>
+__device__ __forceinline__ bool row_ok(const KArgs& a, uint64_t idx, uint64_t cap) {
+  if (!STATS || !ZRT_DEBUG_BOUNDS || idx < cap) return true;
+  atomicOr(a.error_flag, kErrBounds);
+  return false;
+}
 
 // counters[]: progress counters of raytrace.zig:20-34 + traffic diagnostics
 enum { kDepthHits, kReflections, kBackground, kRays, kNodes, kTriTests, kSphereTests, kShades, kTexels,
        kLeaves, kReplays, kExcessTri, kExcessSph, kExcessHits, kNumCounters };
-constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 32;
+constexpr int kWorkSlot = 14, kErrorSlot = 15, kProfSlot = 16, kScratchSlots = 48;
 // STATS flavour, SIMD efficiency (zrt_ctx_debug_counters): traversal loop trips
 // of the waves (per traced step, the most node visits of any lane: kNodes /
 // (64 kTravTrips) is the lane efficiency of traversal), loop iterations in which
@@ -163,6 +181,21 @@ constexpr int kStackOvfWrites = 30;
 // rayColor step, summed over the waves (with kReflections, kBackground and
 // kDepthHits, the steps run: the probe's lane efficiency, auto_sync)
 constexpr int kProbeTrips = 31;
+// STATS: the FAST loops' vector-memory wave-instructions by shape (wave-level
+// event counts, not lane counts): the inputs of bench.py's data-return model
+// (DESIGN.md §4 "The data-return model"), priced per shape by
+// tools/ubench_shapes.hip.  Wave trips that read a global wide node through the
+// vector path (8 dwordx4 loads but for the last: 7) and the distinct nodes they
+// read; trips that read one through the scalar cache; leaf trips that read a
+// node's second refs (one flat dwordx4); wave trips of vector primitive tests and
+// their distinct primitives; scalar primitive tests; shade records read through
+// the vector path; attenuation rows written to / read from global memory.
+// kVNodeCost / kVPrimCost: the same trips' sum of max(16, distinct records) - the
+// data-return cycles of one of their dwordx4 loads (ubench_shapes: 16 per
+// wave-instruction up to 16 distinct 64-B lines, one per line beyond)
+constexpr int kVNodeTrips = 32, kVNodeLines = 33, kSNodeTrips = 34, kRbTrips = 35, kVPrimTrips = 36,
+              kVPrimLines = 37, kSPrimTrips = 38, kVShadeTrips = 39, kAttWTrips = 40, kAttRTrips = 41,
+              kVNodeCost = 42, kVPrimCost = 43;
 
 // ZRT_PROFILE builds (diagnostic only, never the shipped library) add s_memtime
 // cycle sums per loop section into counters[kProfSlot + section].
@@ -1118,8 +1151,27 @@ __device__ __forceinline__ void fill_lds_mats(const KArgs& a, float4* __restrict
 // STATS: coherence of the FAST loop's fetches (kGlobalNodes .. kUniformPrims)
 struct Coh {
   uint32_t gnodes = 0, unodes = 0, ptests = 0, uprims = 0, attw = 0, attr = 0, ovfw = 0;
+  // wave-level events (kVNodeTrips ..), counted in the wave's first active lane
+  uint32_t vn_trips = 0, vn_lines = 0, sn_trips = 0, rb_trips = 0, vp_trips = 0, vp_lines = 0, sp_trips = 0;
+  uint32_t vsh_trips = 0, attw_trips = 0, attr_trips = 0, vn_cost = 0, vp_cost = 0;
   __device__ __forceinline__ void flush(unsigned long long* counters);
 };
+
+// STATS helpers: 1 in the first active lane of the wave (a wave-level event is
+// counted once), and the number of distinct values of x among the active lanes
+__device__ __forceinline__ uint32_t wave_once() {
+  return __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+}
+__device__ __forceinline__ uint32_t wave_distinct(uint32_t x) {
+  uint64_t m = __ballot(1);
+  uint32_t n = 0;
+  while (m != 0ull) {
+    const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(m));
+    m &= ~__ballot(x == f);
+    ++n;
+  }
+  return n;
+}
 
 // One wide node's record in registers: the four slots' near planes, far planes
 // (per axis, pre-swapped in the ray's octant copy) and primitive/child refs.
@@ -1356,7 +1408,8 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
       next = k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3;
     } else if (sp != 0) {
       --sp;
-      next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+      next = kOvf && sp >= rows ? (row_ok<STATS>(a, (uint64_t)(sp - rows) * a.n_lanes + gl, a.ovf_cap) ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : -1)
+                                  : (int32_t)stk[sp * stride];
     }
   } else {
 #endif
@@ -1383,7 +1436,8 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         if (sp + j < rows) {
           stk[(sp + j) * stride] = e[j];
         } else {
-          ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+          if (row_ok<STATS>(a, (uint64_t)(sp + j - rows) * a.n_lanes + gl, a.ovf_cap))
+            ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
           if (STATS) ++coh.ovfw;
         }
       }
@@ -1396,7 +1450,8 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     next = r0;
   } else if (sp != 0) {
     --sp;
-    next = kOvf && sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+    next = kOvf && sp >= rows ? (row_ok<STATS>(a, (uint64_t)(sp - rows) * a.n_lanes + gl, a.ovf_cap) ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : -1)
+                                  : (int32_t)stk[sp * stride];
   }
 #if ZRT_SORT_SKIP
   }
@@ -1409,6 +1464,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
     if (open != 0) {
       const float4 rb = leaf_q[7];
+      if (STATS) coh.rb_trips += wave_once();
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(open);
         open &= open - 1u;
@@ -1426,11 +1482,22 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
         }
         const int fl = __builtin_amdgcn_readfirstlane(L), fb = __builtin_amdgcn_readfirstlane(pb);
         if (ZRT_SCALAR_PRIMS && __ballot(L != fl || pb != fb) == 0ull) {  // one leaf in every active lane
+          if (STATS) coh.sp_trips += wave_once() * (fb != fl ? 2u : 1u);
           prim_test_uniform<true, STATS, ZRT_ORDER_EXACT>(a.prims, fl, r, best_t, best, c_tri, c_sph, lp);
           if (fb != fl) prim_test_uniform<true, STATS, ZRT_ORDER_EXACT>(a.prims, fb, r, best_t, best, c_tri, c_sph, lp);
         } else {
+          if (STATS) {
+            const uint32_t dl = wave_distinct((uint32_t)L);
+            if (wave_once()) { ++coh.vp_trips; coh.vp_lines += dl; coh.vp_cost += max(16u, dl); }
+          }
           prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, L, r, best_t, best, c_tri, c_sph, lp);
-          if (pb != L) prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
+          if (pb != L) {
+            if (STATS) {
+              const uint32_t db = wave_distinct((uint32_t)pb);
+              if (wave_once()) { ++coh.vp_trips; coh.vp_lines += db; coh.vp_cost += max(16u, db); }
+            }
+            prim_test<true, STATS, ZRT_ORDER_EXACT>(a.prims, pb, r, best_t, best, c_tri, c_sph, lp);
+          }
         }
       } while (open != 0);
     }
@@ -1466,6 +1533,7 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
     q = g;
     const uint32_t fa = __builtin_amdgcn_readfirstlane(at);
     if (SCALAR_NODES && __ballot(at != fa) == 0ull) {  // one node in every active lane: scalar loads
+      if (STATS) coh.sn_trips += wave_once();
 #if defined(__HIP_DEVICE_COMPILE__)
       typedef const __attribute__((address_space(4))) float4 cfloat4;
       wide_load(reinterpret_cast<const float4*>((cfloat4*)a.wnodes + fa), sx, sy, sz, w);
@@ -1473,6 +1541,10 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
       wide_load(a.wnodes + fa, sx, sy, sz, w);
 #endif
     } else {
+      if (STATS) {
+        const uint32_t dn = wave_distinct(at);
+        if (wave_once()) { ++coh.vn_trips; coh.vn_lines += dn; coh.vn_cost += max(16u, dn); }
+      }
       wide_load(g, sx, sy, sz, w);
 #if ZRT_AB_DOUBLE_NODE  // A/B probe only (never shipped): the same node read again from another octant copy
       {
@@ -1652,7 +1724,8 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
       next = k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3;
     } else if (sp != 0) {
       --sp;
-      next = sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+      next = sp >= rows ? (row_ok<STATS>(a, (uint64_t)(sp - rows) * a.n_lanes + gl, a.ovf_cap) ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : -1)
+                        : (int32_t)stk[sp * stride];
     }
   } else {
     cswap(k0, r0, k1, r1);
@@ -1674,7 +1747,8 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
           if (sp + j < rows) {
             stk[(sp + j) * stride] = e[j];
           } else {
-            ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
+            if (row_ok<STATS>(a, (uint64_t)(sp + j - rows) * a.n_lanes + gl, a.ovf_cap))
+              ovf[(size_t)(sp + j - rows) * a.n_lanes] = e[j];
             if (STATS) ++coh.ovfw;
           }
         }
@@ -1685,7 +1759,8 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
       next = r0;
     } else if (sp != 0) {
       --sp;
-      next = sp >= rows ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : (int32_t)stk[sp * stride];
+      next = sp >= rows ? (row_ok<STATS>(a, (uint64_t)(sp - rows) * a.n_lanes + gl, a.ovf_cap) ? (int32_t)ovf[(size_t)(sp - rows) * a.n_lanes] : -1)
+                        : (int32_t)stk[sp * stride];
     }
   }
   // each lane walks its candidate leaves in slot order: the record's exact box
@@ -1708,7 +1783,7 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
     SlotT s = slot_interval(__builtin_fmaf(bx, r.ix, -onx) - gx, __builtin_fmaf(by, r.iy, -ony) - gy,
                             __builtin_fmaf(bz, r.iz, -onz) - gz, __builtin_fmaf(cx, r.ix, -ofx) + gx,
                             __builtin_fmaf(cy, r.iy, -ofy) + gy, __builtin_fmaf(cz, r.iz, -ofz) + gz, tb);
-#define ZRT_SURE(S) (__builtin_fmaf(S.en, kFmaSure, Eg) < S.ex)
+#define ZRT_SURE(S) (__builtin_fmaf(S.en, ZRT_FMA_SLABS ? kFmaSure : 1.0f, Eg) < S.ex)
     // (in wide_iter's order: the narrowed test, the per-axis test within the margin,
     // then a sphere slot's static test, which decides it)
     bool o = !deg && !(s.en > __builtin_fmaf(s.ex, rll, sl));
@@ -1721,7 +1796,7 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
 #undef ZRT_SURE
     if (!o) continue;
     const int La = as_int(mn.w), pb = as_int(mx.w);
-    const float lp = ZRT_HAZARD_ENTRY ? __builtin_fmaf(s.en, kFmaSure, E2) : -1.0f;
+    const float lp = ZRT_HAZARD_ENTRY ? (ZRT_FMA_SLABS ? __builtin_fmaf(s.en, kFmaSure, E2) : s.en) : -1.0f;
     if (STATS) {
       const int f = __builtin_amdgcn_readfirstlane(La);
       coh.ptests += 1u;
@@ -1921,6 +1996,18 @@ __device__ __forceinline__ void Coh::flush(unsigned long long* counters) {
   wave_add_u64(&counters[kAttWrites], attw);
   wave_add_u64(&counters[kAttReads], attr);
   wave_add_u64(&counters[kStackOvfWrites], ovfw);
+  wave_add_u64(&counters[kVNodeTrips], vn_trips);
+  wave_add_u64(&counters[kVNodeLines], vn_lines);
+  wave_add_u64(&counters[kSNodeTrips], sn_trips);
+  wave_add_u64(&counters[kRbTrips], rb_trips);
+  wave_add_u64(&counters[kVPrimTrips], vp_trips);
+  wave_add_u64(&counters[kVPrimLines], vp_lines);
+  wave_add_u64(&counters[kSPrimTrips], sp_trips);
+  wave_add_u64(&counters[kVShadeTrips], vsh_trips);
+  wave_add_u64(&counters[kAttWTrips], attw_trips);
+  wave_add_u64(&counters[kAttRTrips], attr_trips);
+  wave_add_u64(&counters[kVNodeCost], vn_cost);
+  wave_add_u64(&counters[kVPrimCost], vp_cost);
 }
 
 // ZRT_FLAG_SCANLINES: a finished unit's counters added to its frame rows.  The
@@ -1991,8 +2078,12 @@ struct AttRows {
 template <bool STATS>
 __device__ __forceinline__ uint32_t att_row(const KArgs& a, const AttRows& ar, uint32_t i, Coh& coh) {
   if (i < a.att_lds_rows) return ar.lds[i * ar.lds_stride];
-  if (STATS) ++coh.attr;
-  return a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index];
+  if (STATS) {
+    ++coh.attr;
+    coh.attr_trips += wave_once();
+  }
+  const uint64_t k = (uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index;
+  return row_ok<STATS>(a, k, a.att_cap) ? a.att[k] : kAttOne;
 }
 #ifndef ZRT_ATT_PAIRS
 #define ZRT_ATT_PAIRS 1  // att_product decodes two rows at a time (their texel loads in flight together)
@@ -2042,6 +2133,7 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
       sh = a.shade[fb];
 #endif
     } else {
+      if (STATS) coh.vsh_trips += wave_once();
       sh = a.shade[best];
     }
     const uint32_t tag = __float_as_uint(sh.w);
@@ -2129,8 +2221,12 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
         if (i < a.att_lds_rows) {
           ar.lds[i * ar.lds_stride] = att;
         } else {
-          a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = att;
-          if (STATS) ++coh.attw;
+          const uint64_t k = (uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index;
+          if (row_ok<STATS>(a, k, a.att_cap)) a.att[k] = att;
+          if (STATS) {
+            ++coh.attw;
+            coh.attw_trips += wave_once();
+          }
         }
       }
       o = loc;
@@ -3254,7 +3350,8 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
           if (i < a.att_lds_rows) {
             ar.lds[i * ar.lds_stride] = att;
           } else {
-            a.att[(uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index] = att;
+            const uint64_t k = (uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index;
+            if (row_ok<STATS>(a, k, a.att_cap)) a.att[k] = att;
             if (STATS) ++coh.attw;
           }
         }
@@ -3824,10 +3921,11 @@ float graze_leaf_margin() {  // ZRT_GRAZE_LEAF: leaf slots' coefficient (A/B of 
 }
 
 // Flatten the scene for the device: BVH (pre-order), slots in DFS leaf order.
-// `device` >= 0: the GPU that may build the BVH (device_bvh).
+// `device` >= 0: the GPU that may build the BVH (device_bvh).  `qnodes`: build
+// the compressed nodes too (1), not (0), or as want_qnodes decides (-1, ZRT_QNODES).
 bool want_qnodes(uint32_t n_wide);
 uint32_t qtop_levels();
-void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
+void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device, int qnodes = -1) {
   const double t0 = now_ms();
   const uint32_t n = s->n_prims;
   std::vector<uint32_t> slot_to_prim, leaf_of_slot;
@@ -3949,7 +4047,7 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
     // also gets compressed nodes stores qtop_levels() (their 64-B nodes leave room
     // for a third level in the path pool's LDS), the full kernels reading the first two
     const uint32_t n_leaf_est = uint32_t(leaves.size());
-    const bool want_q = want_qnodes((n_leaf_est + 2) / 3);  // (the wide tree has about leaves / 3 nodes)
+    const bool want_q = qnodes >= 0 ? qnodes != 0 : want_qnodes((n_leaf_est + 2) / 3);  // (about leaves / 3 nodes)
     const uint32_t top_levels = want_q ? qtop_levels() : 2u;
     const WideBvh wide = build_wide_bvh(leaves, top_levels, ZRT_GROW ? 0.5f * c->graze_m : 0.0f,
                                         ZRT_SPHERE_SLOTS ? sphere_grow : 0.0f, ZRT_SPHERE_SLOTS != 0);
@@ -3973,7 +4071,9 @@ void flatten_scene(HostScene* c, const zrt_scene* s, bool use_bvh, int device) {
 #endif
     c->wide_stack = wide.max_stack + 3;  // + the dead entries of a branch-free push
     // compressed nodes for trees past the caches (want_qnodes): the same tree, 64-B nodes
-    if (want_q) {
+    // (quantize_wide stores octant copies with pre-swapped planes, which wide_iter_q
+    // reads as such: never built for a one-copy A/B build, ZRT_OCT_COPIES = 0)
+    if (want_q && ZRT_OCT_COPIES) {
       const double tq = now_ms();
       QuantWide qw = quantize_wide(wide);
       if (qw.ok) {
@@ -4300,6 +4400,7 @@ struct LdsPlan {
   size_t bytes = 0, budget = 0;
   size_t stack_b = 0, top_b = 0, pool_b = 0, state_b = 0, att_b = 0, mats_b = 0;  // region sizes (check_plan)
 };
+constexpr size_t kLdsPerBlockMax = 160u << 10;  // gfx950: a work-group may use the CU's whole LDS
 // Every region of a plan inside the block's share and disjoint from the others,
 // float4 regions 16-B aligned (the kernels index them from lds_raw by these
 // offsets, nothing else keeps them apart); a violation is a bug in plan_lds.
@@ -4308,6 +4409,9 @@ void check_plan(const LdsPlan& L) {
   const Reg regs[] = {{0, L.stack_b, "stack", false}, {L.top_off, L.top_b, "top nodes", true},
                       {L.pool_off, L.pool_b, "pool", true}, {L.state_off, L.state_b, "lane state", false},
                       {L.att_off, L.att_b, "attenuation rows", false}, {L.mat_off, L.mats_b, "materials", true}};
+  if (L.bytes > kLdsPerBlockMax)
+    throw Error(ZRT_E_UNSUPPORTED, "LDS plan: " + std::to_string(L.bytes) + " B, past a block's " +
+                                       std::to_string(kLdsPerBlockMax) + " B");
   for (const Reg& x : regs) {
     if (!x.n) continue;
     if (x.off + x.n > L.bytes)
@@ -4355,17 +4459,19 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
   want = std::min<uint32_t>(want, max_depth > 1 ? max_depth - 1 : 0);
   LdsPlan L;
   L.budget = budget;
-  if (mode == 3 && (!stk16 || lock)) {
+  if (mode == 3) {
     // the stack takes what the top nodes, the lane state and the wanted attenuation
     // rows leave (the lockstep loop: at most ZRT_STACK_ROWS_LOCK rows; it wants
-    // ZRT_ATT_ROWS_LOCK att rows); deeper rows live in global memory (wide_iter)
+    // ZRT_ATT_ROWS_LOCK att rows); deeper rows live in global memory (wide_iter and
+    // wide_iter_q read them at either stack width, so no FAST plan holds a stack
+    // the block's LDS cannot)
     want = std::min<uint32_t>(want, att_cap);
     const size_t fixed = top + pool_b + state + want * row_att;
     const size_t room = budget > fixed ? budget - fixed : 0;
     L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(stack_depth, uint32_t(room / (kBlock * entry))));
     if (lock) L.stack_rows = std::min<uint32_t>(L.stack_rows, ZRT_STACK_ROWS_LOCK);
   } else {
-    L.stack_rows = stack_depth;  // the whole stack in LDS (the callers check it fits)
+    L.stack_rows = stack_depth;  // BINARY / REFERENCE: the whole stack in LDS (check_plan: within a block's LDS)
   }
   if (const char* f = std::getenv("ZRT_STACK_LDS_ROWS"))  // tests: force the overflow rows into use
     if (mode == 3) L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(L.stack_rows, uint32_t(std::atoi(f))));
@@ -4402,6 +4508,40 @@ LdsPlan plan_lds(const zrt_ctx* c, int mode, bool stk16, uint32_t stack_depth, u
   return plan_lds(node_f4 == kQuantNodeF4 ? c->q_top : c->n_top, c->n_mats, mode, stk16, stack_depth, max_depth, wf,
                   pool, prng, node_f4);
 }
+
+// The context's global buffers that the launches of a frame share (the render
+// launch and its scheduling probe) and that later frames reuse: attenuation rows
+// past the plan's LDS rows ([row][lane], the path pool [row][path]: elements of
+// c->att) and FAST stack rows past the plan's LDS rows ([row][lane]: bytes of
+// c->stack_ovf).  A launch's need follows from its own plan; every launch is
+// checked against the allocation before it is enqueued (check_buffers), so a
+// sizing mistake - round 5's scheduling probe kept 4 LDS attenuation rows where
+// the wavefront render it shared the buffer with kept 12 - is refused as
+// ZRT_E_UNSUPPORTED on the host instead of faulting on the GPU.
+struct BufNeed {
+  uint64_t att_elems = 0;  // u32 attenuation codes
+  uint64_t ovf_bytes = 0;  // stack entries (StackT) past the LDS rows
+};
+BufNeed buffer_need(const LdsPlan& lp, uint32_t max_depth, uint32_t stack_depth, uint64_t n_paths, uint64_t n_lanes,
+                    bool stk16) {
+  BufNeed n;
+  n.att_elems = std::max<uint64_t>(1, max_depth - std::min(max_depth, lp.att_rows)) * n_paths;
+  if (stack_depth > lp.stack_rows)
+    n.ovf_bytes = uint64_t(stack_depth - lp.stack_rows) * n_lanes * (stk16 ? sizeof(uint16_t) : sizeof(uint32_t));
+  return n;
+}
+void check_buffers(const char* launch, const BufNeed& need, uint64_t att_elems, uint64_t ovf_bytes) {
+  if (need.att_elems > att_elems)
+    throw Error(ZRT_E_UNSUPPORTED, std::string(launch) + ": needs " + std::to_string(need.att_elems) +
+                                       " global attenuation-row entries, the context holds " + std::to_string(att_elems));
+  if (need.ovf_bytes > ovf_bytes)
+    throw Error(ZRT_E_UNSUPPORTED, std::string(launch) + ": needs " + std::to_string(need.ovf_bytes) +
+                                       " B of global stack rows, the context holds " + std::to_string(ovf_bytes));
+}
+// The device side of the same check (KArgs::att_cap / ovf_cap: the allocations'
+// elements), in the STATS flavour: a row index past its buffer sets kErrBounds and
+// the access is skipped (tests/test_gpu_runtime.py shrinks the capacity it is told)
+uint64_t ovf_cap_elems(uint64_t ovf_bytes, bool stk16) { return ovf_bytes / (stk16 ? 2u : 4u); }
 
 // Longest-processing-time-first order of this rank's tiles (zrt.h,
 // ZRT_FLAG_NO_SCHEDULE): the probe renders kProbeSpp samples of every tile as
@@ -4456,25 +4596,25 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.lds_pool_off = pp.pool_off;
   pa.lds_state_off = pp.state_off;
   lds = pp.bytes;
-  if (a.stack_depth > pp.stack_rows) {  // its deep stack rows (the render launch's buffer, grown if need be)
-    const uint64_t need = uint64_t(a.stack_depth - pp.stack_rows) * pa.n_lanes * (stk16 ? 2u : 4u);
-    if (c->stack_ovf.n < need) {
+  // its deep stack rows and global attenuation rows ([row][lane] past its LDS rows):
+  // the render launch's buffers, grown if the probe's plan needs more (the wavefront
+  // loop keeps 12 attenuation rows in LDS, the lockstep probe 4)
+  const BufNeed need = buffer_need(pp, a.max_depth, a.stack_depth, pa.n_lanes, pa.n_lanes, stk16);
+  if (need.ovf_bytes) {
+    if (c->stack_ovf.n < need.ovf_bytes) {
       HIPCHK(hipStreamSynchronize(st));  // (the previous launch may still read the old buffer)
-      c->stack_ovf.alloc(need);
+      c->stack_ovf.alloc(need.ovf_bytes);
     }
     a.stack_ovf = pa.stack_ovf = c->stack_ovf.p;
   }
-  // its global attenuation rows, [row][lane] past its LDS rows: the render launch's
-  // buffer, grown if the probe's plan keeps fewer rows in LDS than the render's (the
-  // wavefront loop keeps 12, the lockstep probe 4)
-  {
-    const uint64_t need = std::max<uint64_t>(1, a.max_depth - std::min(a.max_depth, pp.att_rows)) * pa.n_lanes;
-    if (c->att.n < need) {
-      HIPCHK(hipStreamSynchronize(st));  // (the previous launch may still read the old buffer)
-      c->att.alloc(need);
-    }
-    a.att = pa.att = c->att.p;
+  if (c->att.n < need.att_elems) {
+    HIPCHK(hipStreamSynchronize(st));  // (the previous launch may still read the old buffer)
+    c->att.alloc(need.att_elems);
   }
+  a.att = pa.att = c->att.p;
+  a.att_cap = pa.att_cap = c->att.n;
+  a.ovf_cap = pa.ovf_cap = ovf_cap_elems(c->stack_ovf.n, stk16);
+  check_buffers("scheduling probe", need, c->att.n, c->stack_ovf.n);
   HIPCHK(hipMemsetAsync(c->probe_scratch.p, 0, kScratchSlots * sizeof(unsigned long long), st));
   void* fn = prng == ZRT_PRNG_XOSHIRO256 ? probe_ptr<ZRT_PRNG_XOSHIRO256>(stk16)
                                          : probe_ptr<ZRT_PRNG_XOROSHIRO128>(stk16);
@@ -4507,7 +4647,10 @@ int hip_fail(const HipError& e) {
 
 constexpr const char* kOverflowMsg = "BVH traversal stack overflow (tree deeper than the stack was sized for)";
 constexpr const char* kLayoutMsg = "the kernel refused the wide tree: its layout is not the one the kernel decodes";
-const char* device_error_msg(unsigned long long flag) { return (flag & kErrLayout) ? kLayoutMsg : kOverflowMsg; }
+constexpr const char* kBoundsMsg = "a global attenuation or stack row index past its buffer (STATS bounds check)";
+const char* device_error_msg(unsigned long long flag) {
+  return (flag & kErrLayout) ? kLayoutMsg : (flag & kErrBounds) ? kBoundsMsg : kOverflowMsg;
+}
 
 // The device error flag of the context's last launch, copied to pinned host
 // memory behind ev_done.  wait: block until the launch is done and report its
@@ -4773,7 +4916,6 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
-    const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
     const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng, node_f4);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
@@ -4795,10 +4937,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // global attenuation rows: [row][lane], or [path][row] for the path-pool loop
     const uint64_t n_paths = pool ? uint64_t(grid) * zrt::kBlockPaths : n_lanes;
     if (n_paths >= (1ull << 32)) return fail(ZRT_E_UNSUPPORTED, "too many paths");
-    const uint64_t att_need = std::max<uint64_t>(1, p->max_depth - std::min(p->max_depth, lp.att_rows)) * n_paths;
-    if (att_need * sizeof(uint32_t) > (16ull << 30))
+    const zrt::BufNeed need = zrt::buffer_need(lp, p->max_depth, stack_depth, n_paths, n_lanes, stk16);
+    if (need.att_elems * sizeof(uint32_t) > (16ull << 30))
       return fail(ZRT_E_UNSUPPORTED, "max_depth too large for the per-lane attenuation stack");
-    if (c->att.n < att_need) c->att.alloc(att_need);
+    if (c->att.n < need.att_elems) c->att.alloc(need.att_elems);
     HIPCHK(hipMemsetAsync(c->scratch.p, 0, zrt::kScratchSlots * sizeof(unsigned long long), st));
 
     zrt::KArgs a{};
@@ -4864,9 +5006,8 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_qnodes = qn ? c->q_stride / zrt::kQuantNodeF4 : 0u;
     a.n_qleaves = qn ? c->n_qleaves : 0u;
     a.lds_rows = lds_rows;
-    if (stack_depth > lds_rows) {
-      const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
-      if (c->stack_ovf.n < ovf_need) c->stack_ovf.alloc(ovf_need);
+    if (need.ovf_bytes) {
+      if (c->stack_ovf.n < need.ovf_bytes) c->stack_ovf.alloc(need.ovf_bytes);
       a.stack_ovf = c->stack_ovf.p;
     }
     a.n_lanes = uint32_t(n_lanes);
@@ -4923,6 +5064,20 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       if (c->wave_times.n < 2ull * c->n_waves) c->wave_times.alloc(2ull * c->n_waves);
       a.wave_times = c->wave_times.p;
     }
+    // every global row the render launch may touch lies inside its buffer (the probe
+    // may have grown them): checked on the host, and handed to the STATS flavour's
+    // device check
+    zrt::check_buffers("render launch", need, c->att.n, c->stack_ovf.n);
+    a.att = c->att.p;
+    if (need.ovf_bytes) a.stack_ovf = c->stack_ovf.p;
+    a.att_cap = c->att.n;
+    a.ovf_cap = zrt::ovf_cap_elems(c->stack_ovf.n, stk16);
+    if (diag)
+      if (const char* e = std::getenv("ZRT_DEBUG_ROW_CAP")) {  // tests: the device check reports a smaller buffer
+        const double f = std::atof(e);
+        a.att_cap = uint64_t(double(a.att_cap) * f);
+        a.ovf_cap = uint64_t(double(a.ovf_cap) * f);
+      }
     HIPCHK(hipEventRecord(c->ev0, st));
     if (work > 0) {
       void* args[] = {&a};
@@ -5438,7 +5593,6 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     const char* force_rows = std::getenv("ZRT_STACK_LDS_ROWS");  // tests: force the overflow rows into use
     const uint32_t stack_depth = mode == 3 ? std::max(c->wide_stack, c->stack_depth) : c->stack_depth;
     const bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows : c->n_nodes < 65536;
-    const size_t entry = stk16 ? sizeof(uint16_t) : sizeof(uint32_t);
     // FAST over compressed nodes (wide_iter_q, MODE 8) where the context built them
     const bool qn = mode == 3 && c->q_ok;
     const uint32_t node_f4 = qn ? zrt::kQuantNodeF4 : 8u;
@@ -5491,11 +5645,14 @@ int zrt_trace(const zrt_scene* scene, const zrt_params* params, const float* ray
     a.n_top = qn ? c->q_top : c->n_top;
     a.lds_top_off = lp.top_off;
     a.lds_att_off = lp.att_off;
-    if (stack_depth > lds_rows) {
-      const uint64_t ovf_need = uint64_t(stack_depth - lds_rows) * n_lanes * entry;
-      c->stack_ovf.alloc(ovf_need);
+    const zrt::BufNeed need = zrt::buffer_need(lp, 0, stack_depth, n_lanes, n_lanes, stk16);
+    if (need.ovf_bytes) {
+      c->stack_ovf.alloc(need.ovf_bytes);
       a.stack_ovf = c->stack_ovf.p;
     }
+    zrt::check_buffers("trace launch", zrt::BufNeed{0, need.ovf_bytes}, c->att.n, c->stack_ovf.n);
+    a.att_cap = c->att.n;
+    a.ovf_cap = zrt::ovf_cap_elems(c->stack_ovf.n, stk16);
     void* fn = nullptr;
 #define ZRT_TK(M) (stk16 ? reinterpret_cast<void*>(&zrt::trace_kernel<M, uint16_t>) \
                          : reinterpret_cast<void*>(&zrt::trace_kernel<M, uint32_t>))
@@ -5561,7 +5718,9 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
   if (rc) return rc;
   try {
     zrt::HostScene h;
-    zrt::flatten_scene(&h, scene, scene->n_prims > 10, -1);  // (the host BVH build: no device)
+    // (the host BVH build: no device; the compressed nodes built too, so their
+    // plans are checked with the top levels they really keep in LDS)
+    zrt::flatten_scene(&h, scene, scene->n_prims > 10, -1, scene->n_prims > 10 ? 1 : 0);
     const uint32_t n_mats = uint32_t(h.mats.size());
     const uint32_t ref_depth = h.use_bvh ? h.bvh_depth + 2 : 0;
     std::string where;
@@ -5571,12 +5730,17 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
           for (uint32_t prng : {uint32_t(ZRT_PRNG_XOROSHIRO128), uint32_t(ZRT_PRNG_XOSHIRO256)}) {
             for (uint32_t depth : {0u, 1u, 2u, 5u, 20u, 50u}) {
               for (uint32_t nf4 : {8u, 4u}) {  // full / compressed wide nodes (the path pool only)
-                if (nf4 == 4u && loop != 2) continue;
+                if (nf4 == 4u && (loop != 2 || !h.q_ok)) continue;
                 const uint32_t sd = mode == 3 ? std::max(h.wide_stack, ref_depth) : ref_depth;
                 where = "mode " + std::to_string(mode) + " loop " + std::to_string(loop) + " stk16 " +
-                        std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " + std::to_string(depth);
-                (void)zrt::plan_lds(nf4 == 4u ? h.q_top : h.n_top, n_mats, mode, stk16, sd, depth, loop == 1,
-                                    loop == 2, prng, nf4);
+                        std::to_string(int(stk16)) + " prng " + std::to_string(prng) + " depth " +
+                        std::to_string(depth) + " node_f4 " + std::to_string(nf4);
+                try {
+                  (void)zrt::plan_lds(nf4 == 4u ? h.q_top : h.n_top, n_mats, mode, stk16, sd, depth, loop == 1,
+                                      loop == 2, prng, nf4);
+                } catch (const zrt::Error& e) {
+                  throw zrt::Error(e.code, std::string(e.what()) + " (" + where + ")");
+                }
                 ++*n_checked;
               }
             }
@@ -5584,7 +5748,58 @@ int zrt_debug_lds_plans(const zrt_scene* scene, uint32_t* n_checked) {
         }
       }
     }
-    (void)where;
+    return ZRT_OK;
+  }
+  ZRT_CATCH_ALL
+}
+
+int zrt_debug_buffer_plans(const zrt_scene* scene, uint32_t legacy, uint32_t* n_checked) {
+  if (!n_checked) return fail(ZRT_E_INVALID, "null argument");
+  *n_checked = 0;
+  int rc = zrt::validate_scene(scene);
+  if (rc) return rc;
+  if (scene->n_prims <= 10) return ZRT_OK;  // no tree: no FAST launch, no probe
+  try {
+    zrt::HostScene h;
+    zrt::flatten_scene(&h, scene, true, -1, 1);
+    const uint32_t n_mats = uint32_t(h.mats.size());
+    const uint32_t sd = std::max(h.wide_stack, h.bvh_depth + 2);  // zrt_render's FAST stack depth
+    for (int loop = 0; loop < 3; ++loop) {  // the render launch: lockstep, wavefront, path pool
+      for (bool stk16 : {true, false}) {
+        for (uint32_t prng : {uint32_t(ZRT_PRNG_XOROSHIRO128), uint32_t(ZRT_PRNG_XOSHIRO256)}) {
+          for (uint32_t depth : {0u, 1u, 2u, 4u, 5u, 6u, 13u, 20u, 50u}) {
+            for (uint32_t nf4 : {8u, 4u}) {
+              if (nf4 == 4u && (loop != 2 || !h.q_ok)) continue;
+              for (uint32_t grid : {64u, 1536u, 2048u}) {  // blocks (the probe: at most the render's)
+                const std::string where = "loop " + std::to_string(loop) + " stk16 " + std::to_string(int(stk16)) +
+                                          " prng " + std::to_string(prng) + " depth " + std::to_string(depth) +
+                                          " node_f4 " + std::to_string(nf4) + " grid " + std::to_string(grid);
+                // zrt_render's sizing: the render launch's need, then (schedule_tiles) the
+                // probe's, the buffers grown to the larger of the two
+                const zrt::LdsPlan lp = zrt::plan_lds(nf4 == 4u ? h.q_top : h.n_top, n_mats, 3, stk16, sd, depth,
+                                                      loop == 1, loop == 2, prng, nf4);
+                const uint64_t n_lanes = uint64_t(grid) * zrt::kBlock;
+                const uint64_t n_paths = loop == 2 ? uint64_t(grid) * zrt::kBlockPaths : n_lanes;
+                const zrt::BufNeed rn = zrt::buffer_need(lp, depth, sd, n_paths, n_lanes, stk16);
+                const zrt::LdsPlan pp = zrt::plan_lds(h.n_top, n_mats, 3, stk16, sd, depth, false, false, prng, 8);
+                const zrt::BufNeed pn = zrt::buffer_need(pp, depth, sd, n_lanes, n_lanes, stk16);
+                uint64_t att = rn.att_elems, ovf = std::max(rn.ovf_bytes, pn.ovf_bytes);
+                // legacy = 1: the sizing before commit 4072f5f, where the probe shared the
+                // render launch's attenuation rows without growing them
+                if (!legacy) att = std::max(att, pn.att_elems);
+                try {
+                  zrt::check_buffers("scheduling probe", pn, att, ovf);
+                  zrt::check_buffers("render launch", rn, att, ovf);
+                } catch (const zrt::Error& e) {
+                  throw zrt::Error(e.code, std::string(e.what()) + " (" + where + ")");
+                }
+                ++*n_checked;
+              }
+            }
+          }
+        }
+      }
+    }
     return ZRT_OK;
   }
   ZRT_CATCH_ALL
@@ -5597,13 +5812,8 @@ int zrt_debug_qnodes(const zrt_scene* scene, uint64_t* n_checked) {
   if (rc) return rc;
   if (scene->n_prims <= 10) return fail(ZRT_E_INVALID, "no BVH for <= 10 surfaces (raytrace.zig:124-133)");
   try {
-    const char* prev = std::getenv("ZRT_QNODES");
-    const std::string saved = prev ? prev : "";
-    setenv("ZRT_QNODES", "1", 1);
     zrt::HostScene h;
-    zrt::flatten_scene(&h, scene, true, -1);
-    if (prev) setenv("ZRT_QNODES", saved.c_str(), 1);
-    else unsetenv("ZRT_QNODES");
+    zrt::flatten_scene(&h, scene, true, -1, 1);  // (the compressed nodes asked for explicitly)
     if (!h.q_ok) return fail(ZRT_E_UNSUPPORTED, "the encoder refused this tree (a non-finite plane)");
     const uint32_t nn = h.q_stride / zrt::kQuantNodeF4, nw = h.wide_stride / 8u;
     if (nn != nw) return fail(ZRT_E_UNSUPPORTED, "compressed and full trees differ in node count");
