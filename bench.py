@@ -121,74 +121,89 @@ DC_SHAPES = {"vnode_trips": 32, "vnode_lines": 33, "snode_trips": 34, "rb_trips"
 
 
 def shape_costs():
-    """TD (vector data return) busy cycles per wave-instruction of each load shape
-    the render kernel issues, measured alone with the whole chip by
-    tools/ubench_shapes.hip under rocprofv3 (profiles/ubench.json "shapes"): a
-    wave64 dwordx4 load costs 16 cycles (1 KiB of lane data at 64 B/clk) whether
-    its 64 lanes read 1, 2 or 4 records, one cycle per distinct 64-B line beyond
-    16 (64 for 64 lines); a dword per lane (256 B, the scratch layout) costs ~5.7
-    as a load and ~10.7 as a store.  None if the file has no shapes."""
+    """TD (vector data return) cycles per wave-instruction of each load shape the
+    render kernel issues, measured alone with the whole chip by
+    tools/ubench_shapes.hip under rocprofv3 (profiles/ubench.json "shapes"), split
+    into processing (TD_TD_BUSY - TD_TC_STALL) and waiting for the cache
+    (TD_TC_STALL).  A wave64 dwordx4 load takes 16 processing cycles whether its
+    lanes read 1, 2, 4 or 64 records and whether 1 or 64 lanes are active (more
+    distinct lines add TC-stall cycles: one per line past 16); a dword per lane
+    (256 B, the scratch layout) ~4.1 as a load, ~1.9 as a store (+ ~8.8 waiting
+    for the write path).  None if the file has no shapes."""
     try:
         with open(os.path.join(REPO, "profiles", "ubench.json")) as f:
             sh = json.load(f)["shapes"]
     except (OSError, ValueError, KeyError):
         return None
 
-    def td(case):
-        return sh[case]["per_vmem_inst"]["td_busy_cycles_per_cu"]
-    return {"x4": td("node_k1_l2"), "x4_k64": td("node_k64_l2"), "dword_load": td("lane_dwords_load"),
-            "dword_store": td("lane_dwords_store"), "prim_x4": td("prim_k1"),
-            "flat_lds_x4": td("node_lds_flat_k1") if "node_lds_flat_k1" in sh else None,
-            "source": "profiles/ubench.json shapes (tools/ubench_shapes.hip, rocprofv3 --pmc)"}
+    def proc(case):
+        p = sh[case]["per_vmem_inst"]
+        return round(p["td_busy_cycles_per_cu"] - p.get("td_tc_stall_cycles_per_cu", 0.0), 3)
+
+    def stall(case):
+        return sh[case]["per_vmem_inst"].get("td_tc_stall_cycles_per_cu")
+    try:
+        return {"x4": proc("node_k1_l2"), "x4_k64": proc("node_k64_l2"), "prim_x4": proc("prim_k1"),
+                "dword_load": proc("lane_dwords_load"), "dword_store": proc("lane_dwords_store"),
+                "stall": {"x4_k64": stall("node_k64_l2"), "dword_load": stall("lane_dwords_load"),
+                          "dword_store": stall("lane_dwords_store")},
+                "source": "profiles/ubench.json shapes (tools/ubench_shapes.hip, rocprofv3 --pmc): "
+                          "TD_TD_BUSY - TD_TC_STALL per wave-instruction at saturation"}
+    except KeyError:
+        return None
 
 
 def data_return_model(pmc, dc, n_units, kernel_s, clk):
-    """The render launch's vector-memory data-return cycles, modelled (DESIGN.md §4
-    "The data-return model"): the STATS launch's wave-instruction counts per shape
-    (dc: zrt_ctx_debug_counters) x each shape's calibrated cost (shape_costs), plus
-    the vector-memory instructions PMC counts beyond those (scratch: spilled-register
-    reloads and stores, one dword per lane) at the dword costs.  frac = modelled
+    """The render launch's vector-memory data-return (TD) processing cycles,
+    modelled (DESIGN.md §4 "The data-return model"): the STATS launch's wave-
+    instruction counts per load shape (dc: zrt_ctx_debug_counters, DC_SHAPES) x
+    each shape's calibrated processing cycles (shape_costs), plus the vector-memory
+    instructions PMC counts beyond those - scratch (spilled registers' reloads and
+    stores, one dword per lane) - at the dword costs.  frac = modelled processing
     cycles per CU / the launch's cycles: the share of the data-return path's
-    calibrated throughput the launch needs.  Also returned: the model / TD_TD_BUSY
-    ratio (1: the TD busy counter measures throughput; TD_TC_STALL: the part of it
-    spent waiting for the cache)."""
+    calibrated throughput the launch uses.  Checked against the PMC pass: the
+    model over (TD_TD_BUSY - TD_TC_STALL), and the cycles TD spent waiting for the
+    cache (TD_TC_STALL) per launch cycle, reported beside it."""
     c = shape_costs()
     sq, cache = (pmc or {}).get("sq") or {}, (pmc or {}).get("cache") or {}
     if not c or not sq.get("SQ_INSTS_VMEM_RD") or dc is None or len(dc) <= max(DC_SHAPES.values()):
         return None
     n = {k: int(dc[i]) for k, i in DC_SHAPES.items()}
     if not n["vnode_trips"] and not n["snode_trips"]:
-        return None  # not a FAST loop
-    x4 = c["x4"]
-    per_line = (c["x4_k64"] - x4) / 48.0  # cycles per distinct line past 16
+        return None  # not a FAST loop (or a library without the shape counters)
     rd_known = 7 * n["vnode_trips"] + n["rb_trips"] + 3 * n["vprim_trips"] + n["vshade_trips"] + n["att_r_trips"]
     wr_known = n["att_w_trips"] + n_units
     scratch_rd = max(0.0, sq["SQ_INSTS_VMEM_RD"] - rd_known)
     scratch_wr = max(0.0, sq.get("SQ_INSTS_VMEM_WR", 0.0) - wr_known)
     parts = {
-        # 7 dwordx4 per node trip (the 8th, the leaf refs, under rb), max(16, distinct) lines each
-        "node_loads": 7 * (x4 * n["vnode_trips"] + per_line * (n["vnode_cost"] - 16 * n["vnode_trips"])),
-        "leaf_refs": x4 * n["rb_trips"],
-        "prim_loads": 3 * (c["prim_x4"] * n["vprim_trips"] + per_line * (n["vprim_cost"] - 16 * n["vprim_trips"])),
-        "shade_loads": x4 * n["vshade_trips"],
+        "node_loads": 7 * c["x4"] * n["vnode_trips"],  # 7 dwordx4 per vector node trip (the 8th: leaf_refs)
+        "leaf_refs": c["x4"] * n["rb_trips"],
+        "prim_loads": 3 * c["prim_x4"] * n["vprim_trips"],
+        "shade_loads": c["x4"] * n["vshade_trips"],
         "att_rows": c["dword_store"] * n["att_w_trips"] + c["dword_load"] * n["att_r_trips"],
-        "chunk_sums": 4 * c["dword_store"] * n_units,  # one 1 KiB store per unit = 4 x 256 B
+        "chunk_sums": c["x4"] * n_units,  # one dwordx4 store per unit
         "scratch_loads": c["dword_load"] * scratch_rd,
         "scratch_stores": c["dword_store"] * scratch_wr,
     }
     total = sum(parts.values())
     cyc = kernel_s * clk  # the launch's cycles per CU
-    out = {"bound": "vmem_data_return", "cycles_per_launch": float(f"{total:.4e}"),
+    out = {"bound": "vmem_data_return", "processing_cycles_per_launch": float(f"{total:.4e}"),
            "frac": round(total / N_CU / cyc, 4),
            "parts_frac": {k: round(v / N_CU / cyc, 4) for k, v in parts.items()},
            "inputs": {**n, "n_units": int(n_units), "pmc_vmem_rd": sq["SQ_INSTS_VMEM_RD"],
                       "pmc_vmem_wr": sq.get("SQ_INSTS_VMEM_WR"), "scratch_rd_insts": scratch_rd,
                       "scratch_wr_insts": scratch_wr},
-           "costs_td_cycles_per_inst": c}
-    if cache.get("TD_TD_BUSY_sum"):
-        out["model_over_td_busy"] = round(total / cache["TD_TD_BUSY_sum"], 4)
-    if cache.get("TD_TC_STALL_sum") and cache.get("TD_TD_BUSY_sum"):
-        out["td_tc_stall_over_td_busy"] = round(cache["TD_TC_STALL_sum"] / cache["TD_TD_BUSY_sum"], 4)
+           "costs_td_processing_cycles_per_inst": c}
+    busy, stall = cache.get("TD_TD_BUSY_sum"), cache.get("TD_TC_STALL_sum")
+    if busy and stall is not None:
+        out["pmc_processing_frac"] = round((busy - stall) / N_CU / cyc, 4)
+        out["model_over_pmc_processing"] = round(total / (busy - stall), 4)
+        out["pmc_tc_stall_frac"] = round(stall / N_CU / cyc, 4)
+        out["pmc_td_busy_frac"] = round(busy / N_CU / cyc, 4)
+        out["note"] = ("TD busy = processing (the model's rate against the calibrated 16 cycles per dwordx4) + "
+                       "TC stall (TD waiting for the vector cache: L1 misses, the write path)")
+    if cache.get("TCP_TCC_READ_REQ_sum") is not None:
+        out["pmc_l2_read_reqs_per_vmem_rd"] = round(cache["TCP_TCC_READ_REQ_sum"] / sq["SQ_INSTS_VMEM_RD"], 3)
     return out
 
 
@@ -243,9 +258,9 @@ def roofline(pmc, kernel_s, algo_bytes, diag, pmc_reason=None, model_in=None):
         m = data_return_model(pmc, model_in[0], model_in[1], kernel_s, clk)
         if m:
             out["data_return_model"] = m
-            rows["vmem_model"] = {"per_launch": m["cycles_per_launch"],
-                                  "achieved": float(f"{m['cycles_per_launch'] / N_CU / kernel_s:.4e}"),
-                                  "peak": float(f"{clk:.4e}"), "unit": "modelled data-return cycles/s per CU",
+            rows["vmem_model"] = {"per_launch": m["processing_cycles_per_launch"],
+                                  "achieved": float(f"{m['processing_cycles_per_launch'] / N_CU / kernel_s:.4e}"),
+                                  "peak": float(f"{clk:.4e}"), "unit": "modelled TD processing cycles/s per CU",
                                   "frac": m["frac"]}
     if rows:
         # TD_TD_BUSY counts cycles TD is processing OR waiting for data: a utilisation,
@@ -400,7 +415,7 @@ def main_multi(args, devices):
         torch.cuda.synchronize(d)
     elapsed = time.perf_counter() - t0
     frame_sha1 = hashlib.sha1(m.frame().tobytes()).hexdigest()
-    _, diag = m.render(scene.camera, z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS}),
+    _, diag = m.render(scene.camera, z.RenderParams(**{**params.__dict__, "flags": params.flags | z.ZRT_FLAG_STATS}),
                        copy_out=False)
     assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
     m.close()
@@ -483,6 +498,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--traversal", choices=["fast", "reference", "binary"], default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--guard", action="store_true",
+                    help="render with ZRT_FLAG_GUARD (the grazing-triangle guard; the path-pool loop carries it)")
     ap.add_argument("--no-reference-check", action="store_true",
                     help="skip the untimed REFERENCE-traversal launch of the same frame (N=1 only)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -528,7 +545,8 @@ def main():
     trav = {"fast": z.ZRT_TRAVERSAL_FAST, "reference": z.ZRT_TRAVERSAL_REFERENCE,
             "binary": z.ZRT_TRAVERSAL_BINARY}[args.traversal]
     params = z.RenderParams(args.width, args.height, args.spp, args.depth, traversal=trav,
-                            rank=rank, world_size=world, device=local, sample_chunk=args.chunk)
+                            rank=rank, world_size=world, device=local, sample_chunk=args.chunk,
+                            flags=z.ZRT_FLAG_GUARD if args.guard else 0)
     fr = TileFrame(scene, params, rank, world)
 
     for i in range(args.warmup):
@@ -558,7 +576,7 @@ def main():
     frame_sha1 = hashlib.sha1(fr.image().tobytes()).hexdigest() if rank == 0 else None
     # Traffic diagnostics (node visits, primitive tests, ...) come from one extra,
     # untimed launch of the diagnostic kernel flavour: same traversal, same image.
-    diag_kernel_ms = fr.step(z.RenderParams(**{**params.__dict__, "flags": z.ZRT_FLAG_STATS}))
+    diag_kernel_ms = fr.step(z.RenderParams(**{**params.__dict__, "flags": params.flags | z.ZRT_FLAG_STATS}))
     diag = fr.ctx.stats()
     assert diag["rays_processed"] == st["rays_processed"], "diagnostic launch diverged"
     red = "cuda" if args.dist_backend == "nccl" else "cpu"
@@ -623,6 +641,9 @@ def main():
                 wb["pmc_wrreq_32B"] = int(n32)
                 wb["pmc_wrreq_bytes"] = int(64 * n64 + 32 * n32)
         roof["write_budget"] = wb
+        # the STATS launch's vector-load shape counts (data_return_model's inputs), kept in
+        # the line so the model can be recomputed against any PMC entry (tools/dr_model.py)
+        roof["stats_shapes"] = {k: int(dc[i]) for k, i in DC_SHAPES.items()} if len(dc) > 43 else None
         if pe and pe.get("fetch_size_kb") is not None:
             # HBM bytes the sampling loop needs, apart from what spilled registers cost:
             # the measured reads (2 x FETCH_SIZE KiB, MI355X_MICROARCH.md's gfx950
@@ -669,6 +690,7 @@ def main():
                        "scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
                        "max_depth": args.depth, "traversal": args.traversal, "sample_chunk": chunk,
                        "rng": "counter (Xoroshiro128+ per pixel-sample, seed 42)",
+                       "grazing_guard": bool(args.guard),
                        "parallelism": f"image tiles 8x8 round-robin over {world} GPU(s) + RCCL gather"},
             "rays_per_step": int(total_rays),
             "samples_per_step": int(total_samples),

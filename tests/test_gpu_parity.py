@@ -7,11 +7,16 @@ so images and progress counters must be identical — NaN compares equal to NaN.
 
 Run on an MI355X: ``pytest -m gpu``.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
 import zraytrace_amd as z
 from oracle import oracle_py as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -774,9 +779,27 @@ def test_trace_grazing_triangles_unguarded_recorded(scenes, which, monkeypatch):
     o, d = G.grazing_triangle_rays(pr, mins, maxs, left, right, n=20000, seed=1, span=G.scene_span(pr))
     monkeypatch.setenv("ZRT_DEBUG_NO_GUARD", "1")
     _, bad = _trace_all(s.view, o, d, keep=s)
-    print(f"\nscene {which}: unguarded rays differing from the oracle, per traversal: {bad}")
-    assert bad.get(z.ZRT_TRAVERSAL_REFERENCE, 0) == 0  # (the reference's own traversal has no guard to lose)
-    assert all(v <= 20 for v in bad.values()), bad
+    # the counts are persisted, not printed: every run
+    # writes them to gpurun_out/records/grazing_unguarded.json (merged back from the GPU
+    # box; committed as profiles/grazing_unguarded.json), and a count above the
+    # committed one for this scene fails - the gap may shrink, never grow unnoticed
+    names = {z.ZRT_TRAVERSAL_FAST: "fast", z.ZRT_TRAVERSAL_BINARY: "binary", z.ZRT_TRAVERSAL_REFERENCE: "reference"}
+    counts = {names.get(k, str(k)): int(v) for k, v in bad.items()}
+    rec_dir = os.path.join(REPO, "gpurun_out", "records")
+    os.makedirs(rec_dir, exist_ok=True)
+    rec_path = os.path.join(rec_dir, "grazing_unguarded.json")
+    rec = json.load(open(rec_path)) if os.path.exists(rec_path) else {}
+    rec[f"scene{which}"] = {"rays": int(len(o)), "differing_from_oracle": counts, "build_id": z.build_id()}
+    with open(rec_path, "w") as f:
+        json.dump(rec, f, indent=1, sort_keys=True)
+    committed = os.path.join(REPO, "profiles", "grazing_unguarded.json")
+    if os.path.exists(committed):
+        ref = json.load(open(committed)).get(f"scene{which}", {}).get("differing_from_oracle", {})
+        for trav, v in counts.items():
+            if trav in ref:
+                assert v <= ref[trav], f"scene {which} {trav}: {v} differing rays, committed record {ref[trav]}"
+    assert counts.get("reference", 0) == 0  # (the reference's own traversal has no guard to lose)
+    assert all(v <= 20 for v in counts.values()), counts
 
 
 @pytest.mark.parametrize("scene_index,dims", [(4, (128, 128, 8)), (6, (96, 96, 8))], ids=["teapot-balls", "c5-mesh"])

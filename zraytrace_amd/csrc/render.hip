@@ -237,6 +237,9 @@ constexpr int kBlock = 256;
 #ifndef ZRT_LANE_LDS
 #define ZRT_LANE_LDS 1  // lockstep FAST loop: RNG state, chunk sums, sample and depth kept in LDS across the traversal
 #endif
+#ifndef ZRT_LANE_OD
+#define ZRT_LANE_OD 0  // lockstep FAST loop: the ray's origin and direction parked with the lane state too
+#endif
 #ifndef ZRT_STACK_ROWS_LOCK
 #define ZRT_STACK_ROWS_LOCK 16  // lockstep FAST loop: traversal stack rows in LDS (deeper rows in global memory)
 #endif
@@ -643,6 +646,9 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #endif
 #ifndef ZRT_POOL_SCALAR
 #define ZRT_POOL_SCALAR 0  // path-pool loop: a node every traversing lane reads next comes through the scalar cache
+#endif
+#ifndef ZRT_SCALAR_RB
+#define ZRT_SCALAR_RB 0  // FAST: a wave-uniform node's second refs (leaf slots' b refs) through the scalar cache
 #endif
 #ifndef ZRT_SCALAR_PRIMS
 #define ZRT_SCALAR_PRIMS 1  // FAST: a primitive every active lane tests is read through the scalar cache
@@ -1463,8 +1469,26 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if constexpr (sizeof(StackT) == 4 || ZRT_LEAF_LOOP) {
     uint32_t open = (l0 != 0 ? 1u : 0u) | (l1 != 0 ? 2u : 0u) | (l2 != 0 ? 4u : 0u) | (l3 != 0 ? 8u : 0u);
     if (open != 0) {
-      const float4 rb = leaf_q[7];
+      float4 rb;
+#if ZRT_SCALAR_RB && defined(__HIP_DEVICE_COMPILE__)
+      // a node every active lane reads (loaded through the scalar cache, or wave-uniform
+      // anyway): its second refs through the scalar cache too - a vector dwordx4 costs
+      // the data-return path 16 cycles however few lanes or addresses it has
+      // (tools/ubench_shapes.hip)
+      const uint64_t qa = reinterpret_cast<uint64_t>(leaf_q);
+      const uint64_t fq = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(qa >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)qa);
+      if (__ballot(qa != fq) == 0ull && !__builtin_amdgcn_is_shared((const void*)fq)) {
+        typedef const __attribute__((address_space(4))) float4 cfloat4;
+        rb = ((cfloat4*)fq)[7];
+      } else {
+        rb = leaf_q[7];
+        if (STATS) coh.rb_trips += wave_once();
+      }
+#else
+      rb = leaf_q[7];
       if (STATS) coh.rb_trips += wave_once();
+#endif
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(open);
         open &= open - 1u;
@@ -2244,7 +2268,21 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
 template <int PRNG>
 struct LaneState {
   static constexpr uint32_t kRngWords = sizeof(Rng<PRNG>) / 4;
-  static constexpr uint32_t kWords = kRngWords + 5;
+  static constexpr uint32_t kOdWords = ZRT_LANE_OD ? 6 : 0;  // the ray's origin and direction (park_od)
+  static constexpr uint32_t kWords = kRngWords + 5 + kOdWords;
+  __device__ __forceinline__ static void park_od(lds_u32* p, V3 o, V3 d) {
+    const float v[6] = {o.x, o.y, o.z, d.x, d.y, d.z};
+#pragma unroll
+    for (uint32_t k = 0; k < kOdWords; ++k) p[(kRngWords + 5 + k) * kBlock] = __float_as_uint(v[k]);
+  }
+  __device__ __forceinline__ static void unpark_od(const lds_u32* p, V3& o, V3& d) {
+    if (!kOdWords) return;
+    float v[6];
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) v[k] = __uint_as_float(p[(kRngWords + 5 + k) * kBlock]);
+    o = mk(v[0], v[1], v[2]);
+    d = mk(v[3], v[4], v[5]);
+  }
   __device__ __forceinline__ static void park(lds_u32* p, const Rng<PRNG>& rng, float r, float g, float b,
                                               uint32_t sample, uint32_t depth) {
     uint32_t w[kRngWords];
@@ -2454,9 +2492,15 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           }
         }
       } else if (MODE == 3) {
-        if (kLaneLds) LaneState<PRNG>::park(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
+        if (kLaneLds) {
+          LaneState<PRNG>::park(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
+          if (ZRT_LANE_OD) LaneState<PRNG>::park_od(st_l, o, d);
+        }
         traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
-        if (kLaneLds) LaneState<PRNG>::unpark(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
+        if (kLaneLds) {
+          LaneState<PRNG>::unpark(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
+          if (ZRT_LANE_OD) LaneState<PRNG>::unpark_od(st_l, o, d);
+        }
       } else {
         traverse_bvh<MODE == 1, STATS>(a, r, stk, best_t, best, c_nodes, c_tri, c_sph, &excess);
       }
