@@ -12,7 +12,8 @@
 #   smoke                     __graft_entry__.smoke()
 #   adv                       the adversarial exactness tests alone, reported without stopping
 # PYTEST_K: a -k expression for the main test run (e.g. "not near_miss")
-# <cfg>: c2 | c3 | c4 | c5 | c5q (C5 at 1024 spp) | 4k (BASELINE.json configs)
+# <cfg>: c2 | c3 | c3g (C3 with the grazing-triangle guard) | c4 | c5 | c5q (C5 at 1024 spp) | 4k
+#        (BASELINE.json configs)
 # usage: bash tools/gpu_session.sh <tag> [--no-tests] [--no-bench] [step...]
 set -o pipefail
 TAG=$1; shift
@@ -22,6 +23,7 @@ cfg_args() {
   case $1 in
     c2) echo "--scene 1 --width 1000 --height 1000 --spp 1000 --depth 30" ;;
     c3) echo "--scene 3 --width 1024 --height 1024 --spp 256 --depth 20" ;;
+    c3g) echo "--scene 3 --width 1024 --height 1024 --spp 256 --depth 20 --guard" ;;
     c4) echo "" ;;
     c5) echo "--scene 6 --width 4096 --height 4096 --spp 4096 --depth 20 --steps 1 --warmup 0" ;;
     c5q) echo "--scene 6 --width 4096 --height 4096 --spp 1024 --depth 20 --steps 1 --warmup 1" ;;

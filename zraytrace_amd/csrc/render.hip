@@ -314,6 +314,16 @@ template <class R>
 __device__ __forceinline__ bool rand_bool(R& r) {
   return (r.next() & 1u) != 0;
 }
+// r = c ? t : r, word by word (a lane keeps the state it advanced only where it drew)
+template <class R>
+__device__ __forceinline__ void rng_keep(R& r, const R& t, bool c) {
+  uint32_t a[sizeof(R) / 4], b[sizeof(R) / 4];
+  __builtin_memcpy(a, &r, sizeof(a));
+  __builtin_memcpy(b, &t, sizeof(b));
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(R) / 4; ++k) a[k] = c ? b[k] : a[k];
+  __builtin_memcpy(&r, a, sizeof(a));
+}
 
 // ---------------------------------------------------------------------------
 // small vector helpers (evaluation order as vector.zig)
@@ -2109,6 +2119,9 @@ __device__ __forceinline__ uint32_t att_row(const KArgs& a, const AttRows& ar, u
   const uint64_t k = (uint64_t)(i - a.att_lds_rows) * ar.g_stride + ar.g_index;
   return row_ok<STATS>(a, k, a.att_cap) ? a.att[k] : kAttOne;
 }
+#ifndef ZRT_SHADE_CONVERGE
+#define ZRT_SHADE_CONVERGE 0  // BVH loops' shade_step: the operations materials share in Material.scatter issued once
+#endif
 #ifndef ZRT_ATT_PAIRS
 #define ZRT_ATT_PAIRS 1  // att_product decodes two rows at a time (their texel loads in flight together)
 #endif
@@ -2207,6 +2220,124 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
     bool absorbed = false;
     uint32_t att = kAttOne;  // the attenuation as an att code (dielectric: (1, 1, 1))
     V3 nd;
+#if ZRT_SHADE_CONVERGE == 2
+    // as below, every shared piece under a wave-uniform branch (taken when some lane
+    // of the wave needs it) that all the wave's lanes run, each lane keeping its own
+    // result by a select: no divergent branch around the scatter (the divergent form
+    // miscompiled in the 80-VGPR lockstep kernel's timed flavour)
+    {
+      const bool lamb = mkind == ZRT_MAT_LAMBERTIAN, metal = mkind == ZRT_MAT_METAL;
+      const bool diel = !lamb && !metal;
+      V3 ud = d;
+      if (__ballot(!lamb) != 0ull) {
+        const V3 u = unit(d);
+        if (!lamb) ud = u;
+      }
+      float r1 = 0.0f;
+      if (__ballot(lamb) != 0ull) {
+        R t = rng;
+        const float v = rand_float(t);
+        rng_keep(rng, t, lamb);
+        r1 = lamb ? v : 0.0f;
+      }
+      float ratio = 1.0f, cos_theta = 0.0f;
+      if (__ballot(diel) != 0ull) {
+        const float rt = front ? dev::rcp_rn(mat.ior()) : mat.ior();
+        const float ct = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+        ratio = diel ? rt : 1.0f;
+        cos_theta = diel ? ct : 0.0f;
+      }
+      const float qv = lamb ? r1 : cos_theta;
+      const float root = dev::sqrt_rn(1.0f - qv * qv);  // Lambertian rr, dielectric sin_theta
+      bool refl = diel && ratio * root > 1.0f;
+      const bool schlick = diel && !refl;
+      float reflectance = 0.0f;
+      if (__ballot(schlick) != 0ull) {
+        const float r0 = dev::div_rn(1.0f - ratio, 1.0f + ratio);
+        reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+      }
+      const bool draw2 = lamb || schlick;
+      float r2 = 0.0f;
+      if (__ballot(draw2) != 0ull) {
+        R t = rng;
+        const float v = rand_float(t);
+        rng_keep(rng, t, draw2);
+        r2 = draw2 ? v : 0.0f;
+      }
+      refl = schlick ? reflectance > r2 : refl;
+      V3 x = mk(0.0f, 0.0f, 0.0f);
+      if (__ballot(lamb) != 0ull) {
+        float sn, cs;
+        dev::sincos_z(kTwoPi * r2, &sn, &cs);
+        V3 hv = mk(cs * root, sn * root, r1);
+        R t = rng;
+        const bool b = rand_bool(t);
+        rng_keep(rng, t, lamb);
+        if (!b) hv.z = hv.z * -1.0f;
+        const V3 xl = add(normal, hv);
+        if (lamb) x = xl;
+      }
+      const bool rfl = metal || refl, rfr = diel && !refl;
+      if (__ballot(rfl) != 0ull) {
+        const V3 xr = reflect(ud, normal);
+        if (rfl) x = xr;
+      }
+      if (__ballot(rfr) != 0ull) {
+        const V3 xf = refract(ud, normal, ratio);
+        if (rfr) x = xf;
+      }
+      nd = unit(x);
+      if (!diel) att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);
+      if (metal && !(dot(nd, normal) > 0.0f)) absorbed = true;
+    }
+#elif ZRT_SHADE_CONVERGE
+    // the operations the materials share issued once for the lanes of all of them
+    // (shade_hit_a's ZRT_LIST_CONVERGE for the BVH loops): unit(d) of metal and
+    // dielectric, sqrt(1 - q^2) and the second draw of Lambertian and dielectric, the
+    // reflection of metal and reflected dielectric rays, the final unit() of every
+    // scatter and the albedo of Lambertian and metal.  Per lane the same operations on
+    // the same values in the same order: bit-identical.
+    {
+      const bool lamb = mkind == ZRT_MAT_LAMBERTIAN, metal = mkind == ZRT_MAT_METAL;
+      const bool diel = !lamb && !metal;
+      V3 ud = d;
+      if (!lamb) ud = unit(d);
+      float r1 = 0.0f;
+      if (lamb) r1 = rand_float(rng);
+      float ratio = 1.0f, cos_theta = 0.0f;
+      if (diel) {
+        ratio = front ? dev::rcp_rn(mat.ior()) : mat.ior();
+        cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+      }
+      const float qv = lamb ? r1 : cos_theta;
+      const float root = dev::sqrt_rn(1.0f - qv * qv);  // Lambertian rr, dielectric sin_theta
+      bool refl = diel && ratio * root > 1.0f;
+      float reflectance = 0.0f;
+      const bool schlick = diel && !refl;
+      if (schlick) {
+        const float r0 = dev::div_rn(1.0f - ratio, 1.0f + ratio);
+        reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+      }
+      float r2 = 0.0f;
+      if (lamb || schlick) r2 = rand_float(rng);
+      if (schlick) refl = reflectance > r2;
+      V3 x;
+      if (lamb) {
+        float sn, cs;
+        dev::sincos_z(kTwoPi * r2, &sn, &cs);
+        V3 hv = mk(cs * root, sn * root, r1);
+        if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
+        x = add(normal, hv);
+      } else if (metal || refl) {
+        x = reflect(ud, normal);
+      } else {
+        x = refract(ud, normal, ratio);
+      }
+      nd = unit(x);
+      if (!diel) att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);
+      if (metal && !(dot(nd, normal) > 0.0f)) absorbed = true;
+    }
+#else
     if (mkind == ZRT_MAT_LAMBERTIAN) {
       const float r1 = rand_float(rng);
       const float r2 = rand_float(rng);
@@ -2234,6 +2365,7 @@ __device__ __forceinline__ void shade_step(const KArgs& a, const DevMaterial* __
       }
       nd = unit(refl ? reflect(ud, normal) : refract(ud, normal, ratio));
     }
+#endif
     if (absorbed) {
       path_end = true;  // black
     } else {
@@ -3093,6 +3225,9 @@ __device__ __forceinline__ void render_loop_pool(const KArgs& a) {
 #ifndef ZRT_LIST_MERGE
 #define ZRT_LIST_MERGE 1  // list loop: one unit() per step for every new direction (scatters and camera rays)
 #endif
+#ifndef ZRT_LIST_CONVERGE
+#define ZRT_LIST_CONVERGE 1  // list loop: the operations materials share in Material.scatter issued once per wave (C2 +2.9 %, profiles/r06/r06i)
+#endif
 // shade_step's first half for the list loop (ZRT_LIST_MERGE): a hit's scatter up
 // to the direction it normalises.  Every material's new direction - and a new
 // sample's camera ray - is normalised once per step for all lanes together
@@ -3170,6 +3305,55 @@ __device__ __forceinline__ void shade_hit_a(const KArgs& a, const DevMaterial* _
   // metal and dielectric both start from unit(d): one normalisation for the lanes of either
   V3 ud = d;
   if (mkind != ZRT_MAT_LAMBERTIAN) ud = unit(d);
+#if ZRT_LIST_CONVERGE
+  // Material.scatter (material.zig:43-129) with the operations the materials share
+  // issued once for the lanes of all of them (a wave whose lanes hit two or three
+  // materials otherwise runs each shared piece once per material): the correctly
+  // rounded sqrt(1 - q^2) - Lambertian q = its first draw, dielectric q = cos_theta -,
+  // the second uniform draw - Lambertian's r2, the dielectric's reflectance draw,
+  // each lane's draws still in its own order (r1, r2, bool / one draw after its
+  // Schlick term) -, reflect() for metal and reflected dielectric rays, and the
+  // albedo lookup for Lambertian and metal.  The same operations on the same values
+  // per lane as the branches below: bit-identical (test_list_loops_bit_exact).
+  {
+    const bool lamb = mkind == ZRT_MAT_LAMBERTIAN, metal = mkind == ZRT_MAT_METAL;
+    const bool diel = !lamb && !metal;
+    float r1 = 0.0f;
+    if (lamb) r1 = rand_float(rng);
+    float ratio = 1.0f, cos_theta = 0.0f;
+    if (diel) {
+      ratio = front ? dev::rcp_rn(mat.ior()) : mat.ior();
+      cos_theta = dev::fmin_z(dot(neg(ud), normal), 1.0f);
+    }
+    const float qv = lamb ? r1 : cos_theta;
+    const float root = dev::sqrt_rn(1.0f - qv * qv);  // Lambertian rr, dielectric sin_theta
+    bool refl = diel && ratio * root > 1.0f;
+    float reflectance = 0.0f;
+    const bool schlick = diel && !refl;
+    if (schlick) {
+      const float r0 = dev::div_rn(1.0f - ratio, 1.0f + ratio);
+      reflectance = r0 + (1.0f - r0) * dev::pow5_z(1.0f - cos_theta);
+    }
+    float r2 = 0.0f;
+    if (lamb || schlick) r2 = rand_float(rng);
+    if (schlick) refl = reflectance > r2;
+    if (lamb) {
+      float sn, cs;
+      dev::sincos_z(kTwoPi * r2, &sn, &cs);
+      V3 hv = mk(cs * root, sn * root, r1);
+      if (!rand_bool(rng)) hv.z = hv.z * -1.0f;
+      x = add(normal, hv);
+    } else if (metal || refl) {
+      x = reflect(ud, normal);
+    } else {
+      x = refract(ud, normal, ratio);
+    }
+    att = kAttOne;
+    if (!diel) att = albedo_code(mat, tag & 0x7fffffffu, tu, tv);  // (metal: used only when not absorbed)
+    pend = metal ? 2u : 1u;
+    return;
+  }
+#endif
   if (mkind == ZRT_MAT_LAMBERTIAN) {
     const float r1 = rand_float(rng);
     const float r2 = rand_float(rng);
