@@ -2463,7 +2463,15 @@ __device__ __forceinline__ uint32_t auto_sync(const KArgs& a) {
 
 // StackT: uint16_t when the BVH has < 65536 nodes (halves the LDS stack, so
 // more blocks fit per CU), uint32_t otherwise.
-template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT>
+// PROBE: the scheduling probe's instance (schedule_probe_kernel): its one-sample
+// units - one per tile, 65 536 on C4 - are dealt to the waves round-robin instead of
+// through the global counter, whose one atomic per unit serialised the probe
+// (ZRT_PROBE_STATIC; the render launch's units are 32 samples and keep the counter)
+#ifndef ZRT_PROBE_STATIC
+#define ZRT_PROBE_STATIC 1
+#endif
+template <int MODE /*0 list, 1 BVH binary, 2 BVH reference, 3 wide (FAST)*/, int PRNG, bool STATS, class StackT,
+          bool PROBE = false>
 __device__ __forceinline__ void render_loop(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   StackT* stk = reinterpret_cast<StackT*>(lds_raw) + threadIdx.x;  // LDS: the traversal stack
@@ -2505,6 +2513,8 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   ExcessAcc excess;  // REFERENCE traversal, STATS flavour only
 
   uint64_t pf[5] = {0, 0, 0, 0, 0};  // refill, sample start, traversal, shading, path end
+  // (PROBE: this wave's next unit; the waves of the grid take units w, w + W, w + 2W ..)
+  uint32_t probe_u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   uint32_t c_trips = 0, c_loops = 0, c_lsteps = 0, nodes_prev = 0;  // STATS: SIMD efficiency
   for (;;) {
     ++iters;
@@ -2539,8 +2549,13 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           c_depth = c_refl = c_bg = 0;  // (so the launch totals are the rows' sums)
         }
         uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(a.work_counter, 1u);
-        u = __builtin_amdgcn_readfirstlane(u);
+        if (PROBE && ZRT_PROBE_STATIC) {
+          u = probe_u;
+          probe_u += gridDim.x * (kBlock / 64);
+        } else {
+          if (lane == 0) u = atomicAdd(a.work_counter, 1u);
+          u = __builtin_amdgcn_readfirstlane(u);
+        }
         if (u >= a.total_work) break;  // the counter is exhausted
         const uint32_t ord = u / a.n_chunks, g = u - ord * a.n_chunks;
         const uint32_t lt = a.tile_order ? a.tile_order[ord] : ord;  // costliest tiles first
@@ -3661,7 +3676,7 @@ __global__ void __launch_bounds__(kBlock, MODE == 5 || MODE == 7 || MODE == 8 ||
 // symbol so profiles keep it apart from the render launches.
 template <int PRNG, class StackT>
 __global__ void __launch_bounds__(kBlock, ZRT_WAVES_WIDE) schedule_probe_kernel(const KArgs a) {
-  render_loop<3, PRNG, false, StackT>(a);
+  render_loop<3, PRNG, false, StackT, true>(a);
 }
 
 // Closest hit of a batch of rays (zrt_trace): the top-level query of rayColor
