@@ -239,6 +239,7 @@ constexpr int kBlock = 256;
 #endif
 #ifndef ZRT_LANE_OD
 #define ZRT_LANE_OD 0  // lockstep FAST loop: the ray's origin and direction parked with the lane state too
+                       // (25 spills instead of 26; C4 53.6 vs 53.9 Gray/s, profiles/r06/r06c)
 #endif
 #ifndef ZRT_STACK_ROWS_LOCK
 #define ZRT_STACK_ROWS_LOCK 16  // lockstep FAST loop: traversal stack rows in LDS (deeper rows in global memory)
@@ -658,7 +659,8 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #define ZRT_POOL_SCALAR 0  // path-pool loop: a node every traversing lane reads next comes through the scalar cache
 #endif
 #ifndef ZRT_SCALAR_RB
-#define ZRT_SCALAR_RB 0  // FAST: a wave-uniform node's second refs (leaf slots' b refs) through the scalar cache
+#define ZRT_SCALAR_RB 0  // FAST: a wave-uniform node's second refs through the scalar cache (exact; C4 -2.4 %,
+                         // C3 -1.9 %, profiles/r06/r06o: less data-return work, more issue)
 #endif
 #ifndef ZRT_SCALAR_PRIMS
 #define ZRT_SCALAR_PRIMS 1  // FAST: a primitive every active lane tests is read through the scalar cache
@@ -2120,7 +2122,9 @@ __device__ __forceinline__ uint32_t att_row(const KArgs& a, const AttRows& ar, u
   return row_ok<STATS>(a, k, a.att_cap) ? a.att[k] : kAttOne;
 }
 #ifndef ZRT_SHADE_CONVERGE
-#define ZRT_SHADE_CONVERGE 0  // BVH loops' shade_step: the operations materials share in Material.scatter issued once
+#define ZRT_SHADE_CONVERGE 0  // BVH loops' shade_step: the operations materials share in Material.scatter issued
+                              // once (1, 2: exact at 5 waves per SIMD, a wrong frame from the 6-wave lockstep
+                              // kernel's timed flavour - DESIGN.md §3 "The lockstep kernel's spills"; A/B only)
 #endif
 #ifndef ZRT_ATT_PAIRS
 #define ZRT_ATT_PAIRS 1  // att_product decodes two rows at a time (their texel loads in flight together)
