@@ -662,6 +662,9 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #define ZRT_SCALAR_RB 0  // FAST: a wave-uniform node's second refs through the scalar cache (exact; C4 -2.4 %,
                          // C3 -1.9 %, profiles/r06/r06o: less data-return work, more issue)
 #endif
+#ifndef ZRT_LOCK_QN
+#define ZRT_LOCK_QN 0  // A/B: the lockstep FAST loop over the compressed 64-B nodes (wide_iter_q)
+#endif
 #ifndef ZRT_SCALAR_PRIMS
 #define ZRT_SCALAR_PRIMS 1  // FAST: a primitive every active lane tests is read through the scalar cache
 #endif
@@ -1655,7 +1658,7 @@ __device__ __forceinline__ bool static_ok_planes(float bx, float by, float bz, f
   return static_ok(nx, ny, nz, (cx - r.ox) * r.ix, (cy - r.oy) * r.iy, (cz - r.oz) * r.iz);
 }
 
-template <bool STATS, class StackT, bool PAXIS = true, bool GUARD = true>
+template <bool STATS, class StackT, bool PAXIS = true, bool GUARD = true, bool SCALAR = false>
 __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const WideView& v,
                                             StackT* __restrict__ stk, uint32_t gl, WideNodeQ& w,
                                             const float4*& q, uint32_t& sp, float& best_t, int& best,
@@ -1857,8 +1860,19 @@ __device__ __forceinline__ bool wide_iter_q(const KArgs& a, const RayT& r, const
     q = t;
     qnode_load(t, w);
   } else {
-    const float4* __restrict__ g = a.wnodes + (v.base + kQuantNodeF4 * (uint32_t)next);
+    const uint32_t at = v.base + kQuantNodeF4 * (uint32_t)next;
+    const float4* __restrict__ g = a.wnodes + at;
     q = g;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (SCALAR) {  // one node in every active lane (the lockstep loop): scalar loads
+      const uint32_t fa = __builtin_amdgcn_readfirstlane(at);
+      if (__ballot(at != fa) == 0ull) {
+        typedef const __attribute__((address_space(4))) float4 cfloat4;
+        qnode_load((cfloat4*)a.wnodes + fa, w);
+        return true;
+      }
+    }
+#endif
     qnode_load(g, w);
   }
   return true;
@@ -1871,8 +1885,9 @@ __device__ __forceinline__ void node_load(const float4* q, const WideView& v, W&
   else wide_load(q, v.sx, v.sy, v.sz, w);
 }
 
-// zrt_trace over compressed nodes (MODE 8): traverse_wide with wide_iter_q
-template <bool STATS, class StackT>
+// zrt_trace over compressed nodes (MODE 8): traverse_wide with wide_iter_q; LOCK: the
+// lockstep loop's A/B build (ZRT_LOCK_QN: its margins, wave-uniform nodes from the scalar cache)
+template <bool STATS, class StackT, bool LOCK = false>
 __device__ __forceinline__ void traverse_wide_q(const KArgs& a, const RayT& r, StackT* __restrict__ stk,
                                                 const float4* __restrict__ lds_top, uint32_t gl, float& best_t,
                                                 int& best, uint32_t& c_nodes, uint32_t& c_leaves, uint32_t& c_tri,
@@ -1882,8 +1897,8 @@ __device__ __forceinline__ void traverse_wide_q(const KArgs& a, const RayT& r, S
   const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
   WideNodeQ w;
   qnode_load(q, w);
-  while (wide_iter_q<STATS, StackT, true, true>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri,
-                                                c_sph, coh)) {
+  while (wide_iter_q<STATS, StackT, LOCK ? ZRT_PAXIS_LOCK != 0 : true, true, LOCK>(
+      a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
@@ -2647,7 +2662,11 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
           LaneState<PRNG>::park(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
           if (ZRT_LANE_OD) LaneState<PRNG>::park_od(st_l, o, d);
         }
-        traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
+        if constexpr (ZRT_LOCK_QN && !PROBE)
+          traverse_wide_q<STATS, StackT, true>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph,
+                                               c_replays, coh);
+        else
+          traverse_wide<STATS>(a, r, stk, lds_top, gl, best_t, best, c_nodes, c_leaves, c_tri, c_sph, c_replays, coh);
         if (kLaneLds) {
           LaneState<PRNG>::unpark(st_l, rng, acc_r, acc_g, acc_b, sample, depth_left);
           if (ZRT_LANE_OD) LaneState<PRNG>::unpark_od(st_l, o, d);
@@ -4574,7 +4593,7 @@ bool use_pool(const zrt_ctx* c, bool stk16) {
 bool want_qnodes(uint32_t n_wide) {
   if (const char* e = std::getenv("ZRT_QNODES")) return std::atoi(e) != 0;
   (void)n_wide;
-  return false;
+  return ZRT_LOCK_QN != 0;  // (the A/B build's lockstep loop reads nothing else)
 }
 // Top levels of a compressed tree served from LDS (ZRT_QTOP overrides): every ray
 // reads the root and a level-1 node, most a level-2 node - with 64-B nodes the
@@ -5147,8 +5166,11 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     // the grazing-triangle guard (ZRT_FLAG_GUARD): carried by the path-pool loop's traversal
     const bool guard_on = mode == 3 && (p->flags & ZRT_FLAG_GUARD) != 0 && c->guard > 0.0f;
     const bool pool = mode == 3 && p->max_depth >= 1 && (zrt::use_pool(c, stk16) || guard_on);
-    // the path pool over compressed nodes (MODE 8 / 9) where the context built them
-    const bool qn = pool && c->q_ok;
+    // the path pool over compressed nodes (MODE 8 / 9) where the context built them (and
+    // the lockstep loop in the ZRT_LOCK_QN A/B build, which has no other traversal)
+    const bool lock_qn = ZRT_LOCK_QN && mode == 3 && !pool && !wf;
+    if (lock_qn && !c->q_ok) return fail(ZRT_E_UNSUPPORTED, "ZRT_LOCK_QN build: no compressed nodes for this tree");
+    const bool qn = (pool || lock_qn) && c->q_ok;
     const uint32_t node_f4 = qn ? zrt::kQuantNodeF4 : 8u;
     if (pool && stk16) {
       const size_t budget = (160u << 10) / ZRT_WAVES_POOL - (1u << 10);
