@@ -5,7 +5,8 @@
 #   bench:<cfg>               one bench line of config <cfg>
 #   multi:<cfg>:<devices>     bench.py's one-process path (zrt_multi_*) over a device
 #                             list, e.g. multi:c4:0,0 (two ranks rehearsed on GPU 0)
-#   rehearse:<c3|4k>          the N-rank torch.distributed path on one GPU over gloo
+#   rehearse:<c3|4k>[:<n,..>] the N-rank torch.distributed path on one GPU over gloo (rank
+#                             counts, default 2,3; e.g. rehearse:4k:2,8)
 #   ab:<cfg>:<rounds>:<v,..>  interleaved A/B of build variants (abvar/<v>, tools/variants.sh;
 #                             "default" = the shipped library)
 #   envab:<cfg>:<rounds>:<E1|E2..>  interleaved A/B of environment settings (tools/gpu_env_ab.sh)
@@ -48,7 +49,7 @@ for step in "$@"; do
     multi) f=$O/multi_${c}_${a3//,/_}.json
            (cd $R && timeout -k 10 900 python bench.py $(cfg_args $c) --devices $a3 > $f 2> ${f%.json}.err) || { echo "multi $c $a3 failed"; tail -5 ${f%.json}.err; exit 1; }
            python -c "import json; d=json.load(open('$f')); print('multi $c $a3', d['value'], d['ms_per_step'], d['frame_equal_to_n1'], d['per_rank_ms'])" ;;
-    rehearse) bash $R/tools/gpu_rehearse_dist.sh $TAG/dist_$c $c || exit 1 ;;
+    rehearse) bash $R/tools/gpu_rehearse_dist.sh $TAG/dist_$c $c "${a3//,/ }" || exit 1 ;;
     ab) bash $R/tools/ab.sh $TAG/ab_$c $a3 ${a4//,/ } -- --no-reference-check $(cfg_args $c) || exit 1 ;;
     envab) IFS='|' read -ra ENVS <<< "$a4"
            bash $R/tools/gpu_env_ab.sh $TAG/envab_$c $a3 "${ENVS[@]}" -- --no-reference-check $(cfg_args $c) || exit 1 ;;
