@@ -64,6 +64,37 @@ ZRT_UB_VALU(valu_add_u32, "v_add_u32 %0, %0, %1")
 ZRT_UB_VALU(valu_xor_b32, "v_xor_b32 %0, %0, %1")
 ZRT_UB_VALU(valu_rcp_f32, "v_rcp_f32 %0, %0")
 
+// Does scalar work take VALU issue?  The same 16 v_fma_f32 chains with NS scalar ALU
+// instructions per iteration beside them (4 independent SGPR chains): render_kernel
+// issues 0.39 SALU per VALU on C4 (PMC SQ_INSTS_SALU / SQ_INSTS_VALU), mostly exec-mask
+// and uniform-branch work.  If the VALU rate holds as NS grows, SALU is free.
+constexpr int kMixIters = kIters * 4;
+template <int NS>
+__global__ void __launch_bounds__(256) valu_salu_mix(float* out, float a) {
+  float x[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x[k] = threadIdx.x * 0.001f + k;
+  uint32_t s0 = blockIdx.x, s1 = blockIdx.x + 1u, s2 = blockIdx.x + 2u, s3 = blockIdx.x + 3u;
+  for (int i = 0; i < kMixIters; ++i) {  // (milliseconds per launch: ramp-up and launch cost negligible)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x[k]) : "v"(a));
+      if (NS > 0 && (k * NS) % 16 + NS > 15) {  // NS of the 16 slots, spread evenly
+        switch ((k * NS / 16) & 3) {
+          case 0: asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(s0) : : "scc"); break;
+          case 1: asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(s1) : : "scc"); break;
+          case 2: asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(s2) : : "scc"); break;
+          default: asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(s3) : : "scc"); break;
+        }
+      }
+    }
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += x[k];
+  if (s == 12345.678f || (s0 ^ s1 ^ s2 ^ s3) == 0x12345u) out[blockIdx.x] = s;
+}
+
 // float4 loads from a table of `mask + 1` float4 (a power of two), index
 // advancing by `step` float4 per lane and per iteration: with a 16 KiB table
 // every access hits the CU's L1; with a 2 MiB table and a 2 KiB lane stride
@@ -170,6 +201,33 @@ int main() {
       std::printf("  \"%s\": {\"ms\": %.4f, \"wave_insts_per_s\": %.4e, \"per_simd_per_clk_2400\": %.4f}%s\n",
                   ops[o].name, ms, insts / (ms * 1e-3), insts / (ms * 1e-3) / (cus * 4.0) / 2.4e9,
                   o + 1 < nops ? "," : "");
+    }
+    std::printf(" },\n");
+  }
+  {
+    struct {
+      int ns;
+      void (*fn)(float*, float);
+    } mix[] = {{0, valu_salu_mix<0>}, {4, valu_salu_mix<4>}, {8, valu_salu_mix<8>}, {16, valu_salu_mix<16>}};
+    std::printf(" \"valu_salu_mix\": {\n");
+    for (int o = 0; o < 12; ++o) {  // three interleaved rounds of the four mixes
+      hipEvent_t e0, e1;
+      CHK(hipEventCreate(&e0));
+      CHK(hipEventCreate(&e1));
+      hipLaunchKernelGGL(mix[o % 4].fn, dim3(grid), dim3(256), 0, 0, out, 0.999f);
+      CHK(hipDeviceSynchronize());
+      CHK(hipEventRecord(e0));
+      for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(mix[o % 4].fn, dim3(grid), dim3(256), 0, 0, out, 0.999f);
+      CHK(hipEventRecord(e1));
+      CHK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double valu = double(grid) * 4 * kMixIters * 16.0, salu = valu * mix[o % 4].ns / 16.0;
+      std::printf("  \"salu_per_16_valu_%d_r%d\": {\"ms\": %.4f, \"valu_per_simd_per_clk_2400\": %.4f, "
+                  "\"salu_per_simd_per_clk_2400\": %.4f}%s\n",
+                  mix[o % 4].ns, o / 4, ms, valu / (ms * 1e-3) / (cus * 4.0) / 2.4e9,
+                  salu / (ms * 1e-3) / (cus * 4.0) / 2.4e9, o + 1 < 12 ? "," : "");
     }
     std::printf(" },\n");
   }

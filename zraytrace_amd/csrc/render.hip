@@ -652,6 +652,11 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #ifndef ZRT_SORT_SKIP
 #define ZRT_SORT_SKIP 1  // FAST: skip the inner-child sort when no lane of the wave has two children to order
 #endif
+#ifndef ZRT_STACK_LDS_FAST
+#define ZRT_STACK_LDS_FAST 2  // FAST, while every lane's stack is in its LDS rows: 2 the pops as ds_reads in the
+                              // usual branches (C3 +1.6-2.4 %, C4 +0.3 %: profiles/r06/r06w), 1 push / pop as
+                              // LDS selects (A/B: C3 +1.3 %, C4 ±0.3 %), 0 the generic pop only
+#endif
 #ifndef ZRT_SCALAR_NODES
 #define ZRT_SCALAR_NODES 1  // FAST: a wide node every active lane reads next comes through the scalar cache
 #endif
@@ -1421,6 +1426,65 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   float k0 = r0 >= 0 && h0 ? s0.en : inf, k1 = r1 >= 0 && h1 ? s1.en : inf;
   float k2 = r2 >= 0 && h2 ? s2.en : inf, k3 = r3 >= 0 && h3 ? s3.en : inf;
   const uint32_t n = (k0 != inf) + (k1 != inf) + (k2 != inf) + (k3 != inf);
+#if ZRT_STACK_LDS_FAST
+  // every active lane's stack top and its next three pushes inside the LDS rows (a
+  // wave-uniform test, true throughout for trees whose stack fits the LDS plan): the
+  // pop is a ds_read of the lane's LDS column - not a generic load that could also
+  // reach the global rows - and push, pop and the choice between them are selects,
+  // not exec-mask regions (the same stack contents and the same next node)
+  if (ZRT_STACK_LDS_FAST == 2 && __ballot(sp + 3u > rows) == 0ull) {
+    // (A/B form 2: the same branches as below, the pop a ds_read of the LDS column)
+    if (ZRT_SORT_SKIP && __ballot(n > 1u) == 0ull) {
+      if (n != 0) {
+        next = k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3;
+      } else if (sp != 0) {
+        --sp;
+        next = (int32_t)stk[sp * stride];
+      }
+    } else {
+      cswap(k0, r0, k1, r1);
+      cswap(k2, r2, k3, r3);
+      cswap(k0, r0, k2, r2);
+      cswap(k1, r1, k3, r3);
+      cswap(k1, r1, k2, r2);
+      if (n != 0) {
+        stk[sp * stride] = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1);
+        stk[(sp + 1) * stride] = (StackT)(n == 4 ? r2 : r1);
+        stk[(sp + 2) * stride] = (StackT)r1;
+        const uint32_t nsp = sp + n - 1;
+        if (__builtin_expect(nsp > cap - 3, 0)) atomicOr(a.error_flag, kErrOverflow);
+        sp = min(nsp, cap - 3);
+        next = r0;
+      } else if (sp != 0) {
+        --sp;
+        next = (int32_t)stk[sp * stride];
+      }
+    }
+  } else if (ZRT_STACK_LDS_FAST == 1 && __ballot(sp + 3u > rows) == 0ull) {
+    const uint32_t psp = sp != 0 ? sp - 1u : 0u;
+    const int32_t top = (int32_t)stk[psp * stride];
+    if (ZRT_SORT_SKIP && __ballot(n > 1u) == 0ull) {
+      next = n != 0 ? (k0 != inf ? r0 : k1 != inf ? r1 : k2 != inf ? r2 : r3) : sp != 0 ? top : -1;
+      sp = n != 0 ? sp : psp;
+    } else {
+      cswap(k0, r0, k1, r1);
+      cswap(k2, r2, k3, r3);
+      cswap(k0, r0, k2, r2);
+      cswap(k1, r1, k3, r3);
+      cswap(k1, r1, k2, r2);
+      // (a lane with no inner child writes above its top: dead entries)
+      stk[sp * stride] = (StackT)(n == 4 ? r3 : n == 3 ? r2 : r1);
+      stk[(sp + 1) * stride] = (StackT)(n == 4 ? r2 : r1);
+      stk[(sp + 2) * stride] = (StackT)r1;
+      const uint32_t nsp = sp + n - 1;
+      if (__builtin_expect(__ballot(n != 0 && nsp > cap - 3) != 0ull, 0)) {
+        if (n != 0 && nsp > cap - 3) atomicOr(a.error_flag, kErrOverflow);
+      }
+      next = n != 0 ? r0 : sp != 0 ? top : -1;
+      sp = n != 0 ? min(nsp, cap - 3) : psp;
+    }
+  } else {
+#endif
 #if ZRT_SORT_SKIP
   if (__ballot(n > 1u) == 0ull) {
     // every active lane follows at most one inner child: no sort, nothing to push
@@ -1475,6 +1539,9 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
                                   : (int32_t)stk[sp * stride];
   }
 #if ZRT_SORT_SKIP
+  }
+#endif
+#if ZRT_STACK_LDS_FAST
   }
 #endif
   // each lane walks ITS opened leaves in slot order, so lanes that opened
