@@ -652,6 +652,10 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #ifndef ZRT_SORT_SKIP
 #define ZRT_SORT_SKIP 1  // FAST: skip the inner-child sort when no lane of the wave has two children to order
 #endif
+#ifndef ZRT_Q_GLOBAL
+#define ZRT_Q_GLOBAL 0  // lockstep FAST loop: the current node's pointer always its global copy (A/B: exact,
+                        // C4 -0.5 %, C3 +-0, profiles/r06/r06q2)
+#endif
 #ifndef ZRT_STACK_LDS_FAST
 #define ZRT_STACK_LDS_FAST 2  // FAST, while every lane's stack is in its LDS rows: 2 the pops as ds_reads in the
                               // usual branches (C3 +1.6-2.4 %, C4 +0.3 %: profiles/r06/r06w), 1 push / pop as
@@ -1267,7 +1271,8 @@ __device__ __forceinline__ const float4* wide_node_ptr(const KArgs& a, const Wid
 // the order-hazard test of wide_finish follows).  Its state between calls is
 // (w, q, sp, best_t, best) and the lane's stack column, so a traversal can be
 // suspended between nodes (the wavefront loop, render_loop_wf).
-template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK, bool GUARD = true>
+template <bool STATS, class StackT, bool SCALAR_NODES = ZRT_SCALAR_NODES, bool PAXIS = ZRT_PAXIS_LOCK, bool GUARD = true,
+          bool QG = false>
 __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const WideView& v,
                                           StackT* __restrict__ stk, uint32_t gl, WideNode& w,
                                           const float4*& q, uint32_t& sp, float& best_t, int& best,
@@ -1631,7 +1636,9 @@ __device__ __forceinline__ bool wide_iter(const KArgs& a, const RayT& r, const W
   if (next < 0) return false;
   if ((uint32_t)next < v.n_top) {  // a top-level node: from LDS (ds_read)
     const float4* __restrict__ t = v.top + 8u * (uint32_t)next;
-    q = t;
+    // QG: q names the node's global copy even here (the leaf refs and the rare plane
+    // re-reads then load from global memory, never through a generic pointer)
+    q = QG ? a.wnodes + (v.base + 8u * (uint32_t)next) : t;
     wide_load(t, sx, sy, sz, w);
   } else {
     const uint32_t at = v.base + 8u * (uint32_t)next;  // this ray's octant copy
@@ -1978,11 +1985,11 @@ __device__ __forceinline__ void traverse_wide(const KArgs& a, const RayT& r, Sta
   const WideView v = wide_view(a, r, lds_top);
   uint32_t sp = 0;
   // the root is node 0 of this octant's copy (in LDS when the top levels are)
-  const float4* q = ZRT_LDS_TOP ? v.top : a.wnodes + v.base;
+  const float4* q = ZRT_LDS_TOP && !ZRT_Q_GLOBAL ? v.top : a.wnodes + v.base;
   WideNode w;
-  wide_load(q, v.sx, v.sy, v.sz, w);
-  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS>(a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves,
-                                                           c_tri, c_sph, coh)) {
+  wide_load(ZRT_LDS_TOP ? v.top : a.wnodes + v.base, v.sx, v.sy, v.sz, w);
+  while (wide_iter<STATS, StackT, ZRT_SCALAR_NODES, PAXIS, true, ZRT_Q_GLOBAL != 0>(
+      a, r, v, stk, gl, w, q, sp, best_t, best, c_nodes, c_leaves, c_tri, c_sph, coh)) {
   }
   wide_finish<STATS, StackT>(a, r, stk, gl, best_t, best, c_replays);
 }
