@@ -443,6 +443,58 @@ def test_texel_stores_bit_exact():
     assert gs["texel_bytes"] == 12  # one f32 image in the scene
 
 
+def _many_materials_scene(n_side=24):
+    """A grid of n_side^2 small spheres over a ground sphere, every one with a material
+    of its own (lambertian / metal / dielectric in turn, each with a color texture):
+    n_side^2 + 1 materials, 48 B each on the device - past the lockstep and list-lane
+    loops' LDS share (~26 KiB per block) at n_side = 24."""
+    from zraytrace_amd import _ffi
+    import ctypes as C
+    n = n_side * n_side + 1
+    rng = np.random.default_rng(5)
+    cols = rng.random((n, 3), dtype=np.float32)
+    texs = (_ffi.Texture * n)(*[_ffi.Texture(_ffi.ZRT_TEX_COLOR, 0, _ffi.Vec3(*map(float, cols[i])), 0.0, 0.0)
+                                for i in range(n)])
+    kinds = (_ffi.ZRT_MAT_LAMBERTIAN, _ffi.ZRT_MAT_METAL, _ffi.ZRT_MAT_DIELECTRIC)
+    mats = (_ffi.Material * n)(*[_ffi.Material(kinds[i % 3], i, 0.3 if kinds[i % 3] == _ffi.ZRT_MAT_METAL
+                                               else 1.5 if kinds[i % 3] == _ffi.ZRT_MAT_DIELECTRIC else 0.0)
+                                 for i in range(n)])
+    prims = (_ffi.Prim * n)()
+    for i in range(n - 1):
+        gx, gy = i % n_side, i // n_side
+        prims[i].kind = _ffi.ZRT_PRIM_SPHERE
+        prims[i].material = i
+        prims[i].center = _ffi.Vec3(-2.3 + 0.2 * gx, -0.35, 2.0 + 0.2 * gy)
+        prims[i].radius = 0.08
+    prims[n - 1].kind = _ffi.ZRT_PRIM_SPHERE
+    prims[n - 1].material = n - 1
+    prims[n - 1].center = _ffi.Vec3(0.0, -100.5, 3.0)
+    prims[n - 1].radius = 100.0
+    scene = _ffi.Scene(prims, n, n, mats, texs, n, 0, C.cast(None, C.POINTER(_ffi.Image)))
+    scene._keep = (prims, mats, texs)
+    return scene
+
+
+@pytest.mark.parametrize("bvh", [True, False])
+def test_material_table_past_lds_share(bvh):
+    """The lockstep and list-lane loops read the material table from LDS only
+    (ZRT_MATS_LDS_ONLY); a table past their LDS share renders on the loop that reads
+    it from global memory (FAST: the wavefront loop; list: the wave-unit loop), with
+    no tile schedule (its probe is the lockstep loop) - the oracle's frame either way."""
+    import ctypes as C
+    s = _many_materials_scene()
+    cam = z.camera_init((0, 0.6, -1.0), (0, -0.3, 3.0), (0, 1, 0), 50.0, 1.0)
+    p = z.RenderParams(16, 16, 128 if bvh else 4, 6, bounded_volume_hierarchy=bvh)
+    gpu, gs = z.render(C.pointer(s), cam, p)
+    ref, rs = O.render(C.pointer(s), cam, p)
+    assert_bit_exact(gpu, ref)
+    for k in COUNTERS:
+        assert gs[k] == rs[k], k
+    assert gs["sampling_loop"] == (4 if bvh else 0)
+    if bvh:
+        assert gs["schedule_ms"] == 0  # the probe cannot hold the table: tiles in order
+
+
 def test_eight_bit_texels_selected(scenes):
     p = z.RenderParams(8, 8, 1, 2)
     _, gs = z.render(scenes(4), scenes(4).camera, p)

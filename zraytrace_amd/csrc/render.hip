@@ -656,6 +656,13 @@ __device__ __forceinline__ void prim_test(const float4* __restrict__ prims, int 
 #define ZRT_Q_GLOBAL 0  // lockstep FAST loop: the current node's pointer always its global copy (A/B: exact,
                         // C4 -0.5 %, C3 +-0, profiles/r06/r06q2)
 #endif
+#ifndef ZRT_MATS_LDS_ONLY
+// the lockstep and list-lane loops read the material table from their LDS copy only,
+// through LDS-typed pointers (ds_read), not a generic pointer chosen at run time (flat
+// loads); the host plans the table into LDS first and falls back to the wavefront /
+// wave-unit list loop when it does not fit (C4 +1.5 %, C2 +0.5 %: profiles/r06/r06l)
+#define ZRT_MATS_LDS_ONLY 1
+#endif
 #ifndef ZRT_STACK_LDS_FAST
 #define ZRT_STACK_LDS_FAST 2  // FAST, while every lane's stack is in its LDS rows: 2 the pops as ds_reads in the
                               // usual branches (C3 +1.6-2.4 %, C4 +0.3 %: profiles/r06/r06w), 1 push / pop as
@@ -2573,7 +2580,11 @@ __device__ __forceinline__ void render_loop(const KArgs& a) {
   if (MODE == 3 && !layout_ok(a)) return;
   if (MODE == 3 && ZRT_LDS_TOP) fill_lds_top(a, lds_top);
   const DevMaterial* mats = a.mats;
-  if (a.mats_in_lds) {  // block-uniform
+  if (ZRT_MATS_LDS_ONLY && MODE == 3) {  // the host planned the table into LDS: LDS-typed reads
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  } else if (a.mats_in_lds) {  // block-uniform
     float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
     fill_lds_mats(a, m);
     mats = reinterpret_cast<const DevMaterial*>(m);
@@ -3517,7 +3528,11 @@ __device__ __forceinline__ void render_loop_list(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   lds_u32* att_l = (lds_u32*)(lds_raw + a.lds_att_off) + threadIdx.x;  // [row][lane] att codes
   const DevMaterial* mats = a.mats;
-  if (a.mats_in_lds) {  // block-uniform
+  if (ZRT_MATS_LDS_ONLY) {  // the host planned the table into LDS: LDS-typed reads
+    float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
+    fill_lds_mats(a, m);
+    mats = reinterpret_cast<const DevMaterial*>(m);
+  } else if (a.mats_in_lds) {  // block-uniform
     float4* m = reinterpret_cast<float4*>(lds_raw + a.lds_mat_off);
     fill_lds_mats(a, m);
     mats = reinterpret_cast<const DevMaterial*>(m);
@@ -4817,7 +4832,12 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
     if (mode == 3) L.stack_rows = std::max<uint32_t>(1, std::min<uint32_t>(L.stack_rows, uint32_t(std::atoi(f))));
   const size_t stack = (size_t(L.stack_rows) * kBlock * entry + 15) & ~size_t(15);
   const size_t used = stack + top + pool_b + state;
-  L.att_rows = std::min<uint32_t>(want, used < budget ? uint32_t((budget - used) / row_att) : 0u);
+  // loops that read the material table from LDS only (ZRT_MATS_LDS_ONLY): the table
+  // before the attenuation rows, which live in global memory when LDS runs out
+  const size_t mats = size_t(n_mats) * sizeof(DevMaterial);
+  const bool mats_first = ZRT_MATS_LDS_ONLY && (lock || mode == 0);
+  const size_t mats_res = mats_first && used + mats <= budget ? mats : 0;
+  L.att_rows = std::min<uint32_t>(want, used + mats_res < budget ? uint32_t((budget - used - mats_res) / row_att) : 0u);
   L.top_off = uint32_t(stack);
   L.pool_off = uint32_t(stack + top);
   L.state_off = uint32_t(stack + top + pool_b);
@@ -4828,10 +4848,10 @@ LdsPlan plan_lds(uint32_t n_top, uint32_t n_mats, int mode, bool stk16, uint32_t
   L.pool_b = pool_b;
   L.state_b = state;
   L.att_b = L.att_rows * row_att;
-  // the material table, if it fits what is left (ZRT_MATS_LDS=0: A/B, always global)
-  const size_t mats = size_t(n_mats) * sizeof(DevMaterial);
+  // the material table, if it fits what is left (ZRT_MATS_LDS=0: A/B, always global,
+  // for the loops that can read it there)
   const char* me = std::getenv("ZRT_MATS_LDS");
-  if (mats > 0 && L.bytes + mats <= budget && !(me && std::atoi(me) == 0)) {
+  if (mats > 0 && L.bytes + mats <= budget && (mats_first || !(me && std::atoi(me) == 0))) {
     L.mat_off = uint32_t(L.bytes);
     L.mats_in_lds = 1;
     L.bytes += mats;
@@ -4888,7 +4908,7 @@ uint64_t ovf_cap_elems(uint64_t ovf_bytes, bool stk16) { return ovf_bytes / (stk
 // one unit each and records the loop iterations its wave spent (lockstep makes
 // that the unit's time); a stable device radix sort orders the tiles by
 // descending cost, ties in tile order.  Sets a.tile_order for the render launch.
-void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my_tiles, uint32_t grid,
+bool schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my_tiles, uint32_t grid,
                     size_t lds, hipStream_t st) {
   constexpr uint32_t kProbeSpp = ZRT_PROBE_SPP;
   KArgs pa = a;
@@ -4933,6 +4953,9 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   pa.att_lds_rows = pp.att_rows;
   pa.lds_mat_off = pp.mat_off;
   pa.mats_in_lds = pp.mats_in_lds;
+  // (the probe is the lockstep loop, which reads the table from LDS only: no schedule
+  // for a table past its LDS share - the render then takes the tiles in order)
+  if (ZRT_MATS_LDS_ONLY && !pp.mats_in_lds) return false;
   pa.lds_pool_off = pp.pool_off;
   pa.lds_state_off = pp.state_off;
   lds = pp.bytes;
@@ -4967,6 +4990,7 @@ void schedule_tiles(zrt_ctx* c, KArgs& a, uint32_t prng, bool stk16, uint32_t my
   HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(c->sort_temp.p, bytes, c->tile_cost.p, c->cost_sorted.p,
                                                       c->tile_ids.p, c->tile_order.p, int(my_tiles), 0, 32, st));
   a.tile_order = c->tile_order.p;
+  return true;
 }
 
 int hip_fail(const HipError& e) {
@@ -5233,7 +5257,7 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
       stack_depth = std::max<uint32_t>(4, std::min<uint32_t>(stack_depth, uint32_t(std::atoi(cap))));
     bool stk16 = mode == 3 ? c->n_wide < 65536 && c->n_nodes < 65536 && !force_rows : c->n_nodes < 65536;
     // FAST: the wavefront loop (MODE 4) where lanes' traversal lengths diverge
-    const bool wf = mode == 3 && p->max_depth >= 1 && zrt::use_wavefront(c, stk16);
+    bool wf = mode == 3 && p->max_depth >= 1 && zrt::use_wavefront(c, stk16);
     // the path-pool loop (MODE 5) for the same cases, when asked for; a 16-bit stack
     // must fit beside its rays and queues in the block's LDS share, else the 32-bit
     // stack with overflow rows
@@ -5254,12 +5278,23 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     const bool list_lanes = mode == 0 && zrt::use_list_lanes();
     // (the guard's branch costs the path pool 0.7 % on C5, so a guarded render has a
     // kernel of its own, MODE 7; profiles/r04/r04n)
-    const int kmode = pool ? (qn ? (guard_on ? 9 : 8) : (guard_on ? 7 : 5)) : wf ? 4 : list_lanes ? 6 : mode;
-    void* kfn = zrt::select_kernel(kmode, p->prng, diag, stk16);
+    int kmode = pool ? (qn ? (guard_on ? 9 : 8) : (guard_on ? 7 : 5)) : wf ? 4 : list_lanes ? 6 : mode;
     // FAST: deep trees keep their last stack rows in global memory (rarely
     // touched) so the LDS never caps the occupancy the registers allow; the
     // other traversals keep the whole stack in LDS (zrt::plan_lds)
-    const zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng, node_f4);
+    zrt::LdsPlan lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng, node_f4);
+    if (ZRT_MATS_LDS_ONLY && (kmode == 3 || kmode == 6) && !lp.mats_in_lds) {
+      // a material table past the loop's LDS share: the loop that reads it from global
+      // memory (the wavefront loop for FAST, the wave-unit list loop; same images)
+      if (kmode == 6) {
+        kmode = 0;
+      } else {
+        wf = true;
+        kmode = 4;
+      }
+      lp = zrt::plan_lds(c, mode, stk16, stack_depth, p->max_depth, wf, pool, p->prng, node_f4);
+    }
+    void* kfn = zrt::select_kernel(kmode, p->prng, diag, stk16);
     const uint32_t lds_rows = lp.stack_rows;
     const size_t lds = lp.bytes;
     int per_cu = 0;
@@ -5384,10 +5419,10 @@ int zrt_ctx_render_tiles(zrt_ctx* c, const zrt_camera* cam, const zrt_params* p,
     a.n_slots = my_tiles * 64u;
 
     HIPCHK(hipEventRecord(c->ev_pre, st));
-    const bool schedule =
+    bool schedule =
         mode == 3 && !(p->flags & ZRT_FLAG_NO_SCHEDULE) && p->samples_per_pixel >= 128 && my_tiles >= 2;
+    if (schedule) schedule = zrt::schedule_tiles(c, a, p->prng, stk16, my_tiles, grid, lds, st);
     c->scheduled = schedule;
-    if (schedule) zrt::schedule_tiles(c, a, p->prng, stk16, my_tiles, grid, lds, st);
     // the lockstep loop takes its interval from the probe's lane efficiency (auto_sync;
     // ZRT_SYNC or ZRT_AUTO_SYNC=0: the fixed interval, A/B)
     {
