@@ -73,3 +73,20 @@ def test_bound_is_a_rate_not_td_busy():
     assert r["ceilings"]["vmem_td"]["frac"] > r["ceilings"]["valu_issue"]["frac"]  # TD busy reads highest ...
     assert r["bound"] == "valu_issue"  # ... and is not the bound
     assert r["data_return_model"]["frac"] == pytest.approx(r["ceilings"]["vmem_model"]["frac"])
+
+
+def test_ceilings_recomputed_from_committed_files():
+    """tools/dr_model.py --ceilings: the shipped build's C4 bench line (with its
+    roofline) and its PMC entry give back the line's bound and fraction."""
+    import subprocess
+    line = json.loads([x for x in open(os.path.join(REPO, "profiles", "r06", "final", "c4.json"))
+                       if x.startswith("{")][-1])
+    entry = os.path.join(FINAL, "entry.json")
+    assert json.load(open(entry))["build_id"] == line["build_id"]
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "dr_model.py"), "--ceilings",
+                          os.path.join(REPO, "profiles", "r06", "final", "c4.json"), entry],
+                         capture_output=True, text=True, check=True).stdout
+    r = json.loads(out)
+    assert r["bound"] == line["roofline"]["bound"] == "valu_issue"
+    assert r["frac"] == pytest.approx(line["roofline"]["frac"], abs=1e-3)
+    assert r["data_return_model"]["frac"] == pytest.approx(line["roofline"]["data_return_model"]["frac"], abs=1e-3)
